@@ -1,0 +1,256 @@
+#!/usr/bin/env python3
+"""Benchmark of the per-frame ocean path on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg3|cfg2|cfg4|cfg5]
+
+A "step" is one ocean frame: ocean_step(t) = evolve -> 2D IFFT of every plane
+-> fill/foam for every (tile, cascade) unit the rank owns (WaterBody.cs:180-193
+minus GenerateMips), inputs resident in HBM.  Multi-GPU: one process per GPU
+(torchrun), independent oceans (tiles) sharded across ranks -- no data-path
+collective exists; gloo carries only the start/stop barrier and
+the max-over-ranks of the elapsed time.  `value` = ocean-frames of the
+configured ocean (4 x 1024^2 cascades for cfg3) completed per second over all
+ranks.  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ocean-simulation_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (import before ocean_hip: one HIP runtime per process)
+import torch.distributed as dist  # noqa: E402
+
+import ocean_hip as oh  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md (chip-level parameters)
+
+SCENE_PARAMS = dict(wind_speed=8.0, wind_dir_x=1.0, wind_dir_y=-1.0, gravity=9.81, fetch=50000.0, depth=2560.0)
+SCENE_CASCADES = [  # Assets/Scenes/Waves.unity (+ unreferenced 4th cascade :1572-1576)
+    dict(wavelength=1530.0, cutoff_low=1e-10, cutoff_high=1e12, swell=0.4, fade=0.1),
+    dict(wavelength=1000.0, cutoff_low=1e-7, cutoff_high=1e7, swell=0.3, fade=0.2),
+    dict(wavelength=201.0, cutoff_low=1e-5, cutoff_high=1e6, swell=0.1, fade=0.1),
+    dict(wavelength=34.0, cutoff_low=0.001, cutoff_high=10.0, swell=0.4, fade=0.1),
+]
+
+# BASELINE.json configs (tiles are per job; sharded over ranks)
+CONFIGS = {
+    "cfg2": dict(n=512, cascades=1, tiles=1, disp_only=True, per_rank=True,
+                 desc="1 x 512^2 cascade, displacement only"),
+    "cfg3": dict(n=1024, cascades=4, tiles=1, disp_only=False, per_rank=True,
+                 desc="4 x 1024^2 cascades, displacement + derivatives + Jacobian foam"),
+    "cfg4": dict(n=512, cascades=4, tiles=256, disp_only=False, per_rank=False,
+                 desc="256 tiles x 4 x 512^2 cascades, sharded over ranks"),
+    "cfg5": dict(n=4096, cascades=4, tiles=1, disp_only=False, per_rank=True,
+                 desc="4 x 4096^2 cascades"),
+}
+
+
+def algorithmic_bytes(n, units, disp_only):
+    """Per-launch algorithmic HBM bytes.
+    pass A: read h0 + waves (32 B), write P planes (8 B each);
+    pass B: read P planes (8 B each) [+ foam 16 B], write disp 16 B [+ deriv 16 B + turb 16 B]."""
+    tex = n * n * units
+    if disp_only:
+        return {"pass_a": tex * (32 + 16), "pass_b": tex * (16 + 16), "frame": tex * 80}
+    return {"pass_a": tex * (32 + 32), "pass_b": tex * (32 + 16 + 48), "frame": tex * 160}
+
+
+def cpu_baseline(cfg, frames=3):
+    """Scalar single-thread C port of the reference path (oracle/ocean_oracle.c), full frame
+    (evolve + radix-2 IFFT of every plane + fill) on the host cores of this box."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    n, C = cfg["n"], cfg["cascades"]
+    if n > 1024:  # bound the CPU sample (~10-30 s): time 1024^2 cascades and scale by texel count x log2N
+        n_s = 1024
+    else:
+        n_s = n
+    noise = O.generate_noise(n_s, 20251121)
+    oc = O.OracleOcean(n_s, SCENE_PARAMS, SCENE_CASCADES[:C], noise, nplanes=2 if cfg["disp_only"] else 4)
+    oc.step(0.0)  # warm-up
+    ts = []
+    for f in range(frames):
+        t0 = time.perf_counter()
+        oc.step((f + 1) / 60.0)
+        ts.append(time.perf_counter() - t0)
+    sec = float(np.median(ts))
+    scale = (n * n * np.log2(n)) / (n_s * n_s * np.log2(n_s))
+    sec *= scale
+    per_tile = 1.0 / sec
+    return {"value": per_tile, "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"median of {frames} frames after 1 warm-up, 1 ocean of {C} x {n_s}^2 "
+                      f"{'(scaled x%.2f to %d^2) ' % (scale, n) if scale != 1 else ''}"
+                      f"on 1 host core; C port of the reference path (oracle/ocean_oracle.c); "
+                      f"the C# scalar baseline of north_star needs dotnet, absent on this image"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
+    ap.add_argument("--unfused", action="store_true", help="reference-shaped schedule (evolve, 4 x ifft2d, fill)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ifft-stage", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    if args.gpus != world and not (world == 1 and args.gpus == 1):
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+
+    cfg = CONFIGS[args.config]
+    n, C = cfg["n"], cfg["cascades"]
+    if cfg["per_rank"]:
+        tiles = cfg["tiles"]  # each rank runs its own ocean(s): weak scaling over independent oceans
+    else:
+        tiles = cfg["tiles"] // world + (1 if rank < cfg["tiles"] % world else 0)
+    flags = (oh.F_DISPLACEMENT_ONLY if cfg["disp_only"] else 0) | (oh.F_UNFUSED if args.unfused else 0)
+
+    torch.cuda.set_device(local)
+    ctx = oh.OceanContext(n, C, tiles, flags, device=local)
+    ctx.set_params(SCENE_PARAMS, SCENE_CASCADES[:C])
+    ctx.generate_noise(20251121 + rank * max(tiles, 1))
+    ctx.init_spectrum()
+    ctx.synchronize()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    # warm-up
+    for f in range(args.warmup):
+        ctx.step(f / 60.0)
+    ctx.synchronize()
+
+    # timed region: per-kernel HIP events on the ctx stream (ocean_set_kernel_timing)
+    ctx.set_kernel_timing(True)
+    ctx.kernel_stats(0), ctx.kernel_stats(1), ctx.kernel_stats(2)  # reset
+    barrier()
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for f in range(args.steps):
+        ctx.step((args.warmup + f) / 60.0)
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    ka_ms, ka_n = ctx.kernel_stats(0)
+    kb_ms, kb_n = ctx.kernel_stats(1)
+    ctx.set_kernel_timing(False)
+
+    # same region without per-kernel events (event overhead check)
+    ctx.synchronize()
+    t2 = time.perf_counter()
+    for f in range(args.steps):
+        ctx.step((args.warmup + args.steps + f) / 60.0)
+    ctx.synchronize()
+    t3 = time.perf_counter()
+    elapsed_noev = t3 - t2
+
+    if world > 1:
+        tt = torch.tensor([elapsed, elapsed_noev], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed, elapsed_noev = float(tt[0]), float(tt[1])
+        tot = torch.tensor([tiles], dtype=torch.float64)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        total_tiles = int(tot[0])
+    else:
+        total_tiles = tiles
+
+    units = tiles * C
+    B = algorithmic_bytes(n, units, cfg["disp_only"])
+    a_us = 1e3 * ka_ms / max(ka_n, 1)
+    b_us = 1e3 * kb_ms / max(kb_n, 1)
+    dom, dom_us = ("pass_b", b_us) if b_us >= a_us else ("pass_a", a_us)
+    if args.unfused:
+        dom = "ifft_cols" if dom == "pass_b" else "ifft_rows"
+    dom_bytes = B["pass_b" if dom in ("pass_b", "ifft_cols") else "pass_a"]
+    if args.unfused:  # unfused row/col kernels move 16 B per texel per plane
+        dom_bytes = n * n * units * 16
+    achieved = dom_bytes / (dom_us * 1e-6) / 1e9 if dom_us > 0 else 0.0
+
+    ifft_stage = None
+    if not args.no_ifft_stage and not cfg["disp_only"]:
+        # operator-level stage (IFFT.InverseFastFourierTransform x 4 planes), unfused kernels
+        ctx.set_kernel_timing(True)
+        ctx.kernel_stats(0), ctx.kernel_stats(1), ctx.kernel_stats(2)
+        reps = max(20, args.steps // 5)
+        ctx.synchronize()
+        s0 = time.perf_counter()
+        for _ in range(reps):
+            ctx.ifft2d(0b1111)
+        ctx.synchronize()
+        s1 = time.perf_counter()
+        r_ms, r_n = ctx.kernel_stats(0)
+        c_ms, c_n = ctx.kernel_stats(1)
+        ctx.set_kernel_timing(False)
+        fft_bytes = 32 * n * n * 4 * units
+        stage_us = 1e6 * (s1 - s0) / reps
+        kern_us = 1e3 * (r_ms + c_ms) / reps
+        ifft_stage = {"bytes": fft_bytes, "us_per_stage_wall": round(stage_us, 2),
+                      "us_per_stage_kernels": round(kern_us, 2),
+                      "row_kernel_us": round(1e3 * r_ms / max(r_n, 1), 2),
+                      "col_kernel_us": round(1e3 * c_ms / max(c_n, 1), 2),
+                      "achieved_GBs": round(fft_bytes / (kern_us * 1e-6) / 1e9, 1),
+                      "frac": round(fft_bytes / (kern_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(cfg)
+
+    if rank == 0:
+        frames = args.steps * total_tiles  # ocean-frames (one frame of one ocean = C cascades of N^2)
+        value = frames / elapsed
+        out = {
+            "metric": "ocean-surface frames/sec (4x1024^2 cascades)" if args.config == "cfg3"
+            else f"ocean-surface frames/sec ({cfg['desc']})",
+            "value": round(value, 2),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (scene parameters of Waves.unity, seeded noise 20251121+tile)",
+            "config": {"workload": f"{args.config}: {cfg['desc']}", "n": n, "cascades": C,
+                       "tiles_per_gpu": tiles, "tiles_total": total_tiles,
+                       "schedule": "unfused" if args.unfused else "fused (pass A + pass B)",
+                       "parallelism": f"independent oceans sharded over {world} GPU(s), no collective"},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_us": round(dom_us, 3)},
+            "kernels_us": {"pass_a" if not args.unfused else "rows": round(a_us, 3),
+                           "pass_b" if not args.unfused else "cols": round(b_us, 3)},
+            "frame": {"algorithmic_bytes": B["frame"],
+                      "achieved_GBs": round(B["frame"] * tiles / max(tiles, 1) / (elapsed / args.steps) / 1e9, 1),
+                      "ms_per_step_without_kernel_events": round(1e3 * elapsed_noev / args.steps, 5)},
+            "ifft_stage": ifft_stage,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

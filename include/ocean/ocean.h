@@ -1,0 +1,182 @@
+/*
+ * ocean.h -- C ABI of liboceanhip.so, the MI355X (gfx950) implementation of the
+ * reference's per-frame Tessendorf ocean path (Mozobo/Ocean-Simulation).
+ *
+ * The reference boundary is Unity's ComputeShader binding API driven from C#:
+ * WaterBody.cs binds textures/buffers by string name and Dispatch()es the
+ * InitialSpectrum / TimeDependentSpectrum / IFFT / ResultTexturesFiller kernels,
+ * and the output stays in Tex2DArray RenderTextures read by Water.shader and by
+ * AsyncGPUReadback (WaterBody.cs:180-193, :288-296).  Each entry point below
+ * names the reference interface it replaces.  A C# P/Invoke binding of every
+ * symbol is given in INTEGRATION.md.
+ *
+ * Conventions
+ *   - cdecl, every struct blittable (LayoutKind.Sequential in C#).
+ *   - Every int-returning call returns OCEAN_OK (0) or a negative OCEAN_E_*;
+ *     no C++ exception crosses the ABI.  ocean_last_error() gives a
+ *     thread-local message for the last failure on the calling thread.
+ *   - The context owns all device memory; the caller owns host buffers, which
+ *     are only read/written during the call.
+ *   - GPU work is enqueued on the context's own HIP stream (one per ctx); only
+ *     ocean_read / ocean_write / ocean_synchronize / ocean_set_noise /
+ *     ocean_generate_noise block the calling thread.
+ *   - A context is not thread-safe: drive it from one thread (like Unity's
+ *     main thread).  Multi-GPU = one context per device.
+ *
+ * Memory layout in HBM (all fp32, texture index = [unit][y][x], unit = tile*C + cascade,
+ * matching Unity's Tex2DArray [slice][y][x] with id.x = x):
+ *   NOISE  float2 [T][N][N]       H0    float4 [T*C][N][N]   WAVES float4 [T*C][N][N]
+ *   PLANEp float2 [T*C][N][N]     p = 0 DxDz, 1 DyDxz, 2 DyxDyz, 3 DxxDzz
+ *   DISP   float4 [T*C][N][N]     DERIV float4 [T*C][N][N]  TURB  float4 [T*C][N][N]
+ *   NORMAL float4 [T*C][N][N]     (derived output, OCEAN_F_NORMALS only)
+ */
+#ifndef OCEAN_OCEAN_H
+#define OCEAN_OCEAN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OCEAN_ABI_VERSION 1
+
+/* status codes */
+#define OCEAN_OK 0
+#define OCEAN_E_INVALID_ARG (-1)   /* bad pointer, size, index or enum */
+#define OCEAN_E_UNSUPPORTED (-2)   /* N not a power of two in [16, 4096], C not in [1, 5], ... */
+#define OCEAN_E_STATE (-3)         /* call order violated (e.g. step before init_spectrum) */
+#define OCEAN_E_DEVICE (-4)        /* HIP runtime / kernel launch failure */
+#define OCEAN_E_OUT_OF_MEMORY (-5) /* hipMalloc failed */
+
+/* ocean_create flags */
+#define OCEAN_F_DISPLACEMENT_ONLY 0x1u /* 2 planes (DxDz, DyDxz) -> DISP only (BASELINE cfg2) */
+#define OCEAN_F_NORMALS 0x2u           /* also write the per-cascade NORMAL texture (Water.shader:346-348) */
+#define OCEAN_F_UNFUSED 0x4u           /* ocean_step runs the reference-shaped schedule:
+                                          evolve -> 4 x ifft2d -> fill (WaterBody.cs:180-190) */
+
+/* texture ids for ocean_read / ocean_write / ocean_get_device_ptr */
+enum ocean_texture {
+    OCEAN_TEX_NOISE = 0,  /* _RandomNoiseTexture           WaterBody.cs:86-100 (per tile, cascade ignored) */
+    OCEAN_TEX_H0 = 1,     /* _InitialSpectrumTextures      InitialSpectrum.compute:14 */
+    OCEAN_TEX_WAVES = 2,  /* _WavesDataTextures            InitialSpectrum.compute:15 */
+    OCEAN_TEX_PLANE0 = 3, /* _DxDzTextures                 TimeDependentSpectrum.compute:6 */
+    OCEAN_TEX_PLANE1 = 4, /* _DyDxzTextures */
+    OCEAN_TEX_PLANE2 = 5, /* _DyxDyzTextures */
+    OCEAN_TEX_PLANE3 = 6, /* _DxxDzzTextures */
+    OCEAN_TEX_DISP = 7,   /* _DisplacementsTextures        ResultTexturesFiller.compute:7 */
+    OCEAN_TEX_DERIV = 8,  /* _DerivativesTextures          ResultTexturesFiller.compute:8 */
+    OCEAN_TEX_TURB = 9,   /* _TurbulenceTextures (foam state) ResultTexturesFiller.compute:9 */
+    OCEAN_TEX_NORMAL = 10 /* derived: normalize(-Dyx/(1+Dxx), 1, -Dyz/(1+Dzz)), w = 0 */
+};
+
+typedef struct ocean_ctx ocean_ctx;
+
+/* WaterBody public ocean parameters, WaterBody.cs:10-14. */
+typedef struct ocean_params {
+    float wind_speed;
+    float wind_dir_x;
+    float wind_dir_y;
+    float gravity;
+    float fetch;
+    float depth;
+} ocean_params;
+
+/* WaterCascade component, WaterCascade.cs:10-24 (flattened as WaterBody.cs:231-242). */
+typedef struct ocean_cascade {
+    float wavelength; /* patch length L */
+    float cutoff_low;
+    float cutoff_high;
+    float swell;
+    float fade;
+} ocean_cascade;
+
+/* Replaces WaterBody.Awake resource creation (WaterBody.cs:211-251) and
+ * new IFFT(...) (IFFT.cs:24-62): allocates every texture for `n_tiles`
+ * independent oceans of `n_cascades` cascades at N = `n` on HIP device
+ * `device`, and builds the twiddle table.  16 <= n <= 4096, power of two;
+ * 1 <= n_cascades <= 5 (Water.shader:139); n_tiles >= 1. */
+int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags, ocean_ctx **out);
+
+/* Replaces OnDisable (WaterBody.cs:300-309) + RT release.  NULL is a no-op. */
+void ocean_destroy(ocean_ctx *ctx);
+
+/* Replaces the SetFloat/SetBuffer parameter bindings of
+ * InitializeInitialSpectrumComputeShader (WaterBody.cs:130-148).
+ * `cascades` has n_cascades entries.  Takes effect at the next ocean_init_spectrum. */
+int ocean_set_params(ocean_ctx *ctx, const ocean_params *params, const ocean_cascade *cascades);
+
+/* Replaces GenerateRandomNoiseTexture + Texture2D.Apply (WaterBody.cs:86-100, :97):
+ * uploads tile `tile`'s noise, float2[N][N] laid out [y][x] (g1, g2). Blocking. */
+int ocean_set_noise(ocean_ctx *ctx, int tile, const float *rg);
+
+/* This library's documented, seeded noise (the reference's UnityEngine.Random is
+ * unseeded and closed): tile t uses seed + t; Marsaglia polar over xorshift128
+ * seeded by splitmix64, texels generated x-outer / y-inner, g1 then g2
+ * (WaterBody.cs:71-100).  Generated on the host, uploaded.  Blocking. */
+int ocean_generate_noise(ocean_ctx *ctx, uint64_t seed);
+
+/* Replaces CalculateInitialSpectrumTextures (WaterBody.cs:171-178):
+ * InitialSpectrum.compute:99-129 then :135-143 for every tile and cascade.
+ * Also zeroes the foam state (TURB).  Async on the ctx stream. */
+int ocean_init_spectrum(ocean_ctx *ctx);
+
+/* Replaces CalculateWavesTexturesAtTime(time) (WaterBody.cs:180-193, minus
+ * GenerateMips): evolve -> 2D IFFT of every plane -> fill/foam for all tiles
+ * and cascades.  Async on the ctx stream.  Fused 2-kernel schedule by default;
+ * OCEAN_F_UNFUSED selects the reference-shaped one (same results to rounding). */
+int ocean_step(ocean_ctx *ctx, float time);
+
+/* Replaces the TimeDependentSpectrum dispatch alone (WaterBody.cs:181-182;
+ * TimeDependentSpectrum.compute:20-47): writes PLANE0..3 at `time`.  Async. */
+int ocean_evolve(ocean_ctx *ctx, float time);
+
+/* Replaces IFFT.InverseFastFourierTransform(RenderTexture) (IFFT.cs:66-94) for
+ * every plane p with bit p set in `plane_mask`: in place,
+ * out[m] = (-1)^(mx+my) * sum_{x,y} in[x,y] e^{+2 pi i (x mx + y my)/N}
+ * over all tiles and cascades.  Async. */
+int ocean_ifft2d(ocean_ctx *ctx, int plane_mask);
+
+/* Replaces the FillResultTextures dispatch (WaterBody.cs:189;
+ * ResultTexturesFiller.compute:16-34): PLANE0..3 + TURB -> DISP, DERIV, TURB.  Async. */
+int ocean_fill(ocean_ctx *ctx);
+
+/* Synchronous texture readback of one (tile, cascade) slice, replacing
+ * AsyncGPUReadback.Request(...).GetData<Color>() (WaterBody.cs:288-296).
+ * `bytes` must equal the slice size (N*N*16 for float4, N*N*8 for float2).
+ * Orders after all work queued on the ctx stream. */
+int ocean_read(ocean_ctx *ctx, int texture, int tile, int cascade, void *dst, size_t bytes);
+
+/* Synchronous upload of one slice (foam state for resume, planes for
+ * operator-level tests).  Same size rules as ocean_read. */
+int ocean_write(ocean_ctx *ctx, int texture, int tile, int cascade, const void *src, size_t bytes);
+
+/* Zero-copy access for same-process consumers: base device pointer and total
+ * byte size of a texture (all tiles and cascades). */
+int ocean_get_device_ptr(ocean_ctx *ctx, int texture, void **ptr, size_t *bytes);
+
+/* The ctx's hipStream_t (as void*), for callers that order their own work. */
+int ocean_get_stream(ocean_ctx *ctx, void **stream);
+
+/* Blocks until all work queued on the ctx stream has finished. */
+int ocean_synchronize(ocean_ctx *ctx);
+
+/* Kernel timing: when enabled, each kernel launch of ocean_step / ocean_ifft2d
+ * is bracketed by HIP events on the ctx stream; ocean_kernel_stats returns, for
+ * kernel `kind` (0 = pass A / row pass, 1 = pass B / column pass, 2 = other),
+ * the summed duration in ms and the launch count since the last reset
+ * (synchronizes the stream). */
+int ocean_set_kernel_timing(ocean_ctx *ctx, int enable);
+int ocean_kernel_stats(ocean_ctx *ctx, int kind, double *total_ms, long long *launches);
+
+/* Thread-local message describing the last failure on this thread ("" if none). */
+const char *ocean_last_error(void);
+
+/* OCEAN_ABI_VERSION of the loaded library. */
+int ocean_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OCEAN_OCEAN_H */

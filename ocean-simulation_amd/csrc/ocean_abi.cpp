@@ -1,0 +1,454 @@
+// C-ABI layer of liboceanhip.so: context lifetime, validation, device memory,
+// the per-frame schedule, readback and kernel timing.  See include/ocean/ocean.h
+// for the reference interface each entry point replaces.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "ocean_internal.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    return fail(OCEAN_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define OCEAN_HIP(call)                                   \
+    do {                                                  \
+        hipError_t _e = (call);                           \
+        if (_e != hipSuccess) return hip_fail(_e, #call); \
+    } while (0)
+
+struct TimedLaunch {
+    int kind;
+    hipEvent_t a, b;
+};
+
+}  // namespace
+
+// Host noise generator (WaterBody.cs:71-100 with this library's documented
+// uniform source).  Defined in noise.cpp.
+namespace ocean {
+void generate_noise_host(int n, uint64_t seed, float* out);
+}
+
+struct ocean_ctx {
+    int device = 0;
+    int n = 0, logn = 0, C = 0, T = 0, P = 4;
+    uint32_t flags = 0;
+    hipStream_t stream = nullptr;
+    // device buffers
+    float2* noise = nullptr;
+    float4* h0 = nullptr;
+    float4* waves = nullptr;
+    float2* plane[4] = {nullptr, nullptr, nullptr, nullptr};
+    float4* disp = nullptr;
+    float4* deriv = nullptr;
+    float4* turb = nullptr;
+    float4* normal = nullptr;
+    float2* tw = nullptr;
+    float* casc = nullptr;
+    // host state
+    ocean::SpectrumParams params{};
+    bool params_set = false;
+    std::vector<bool> noise_set;
+    bool spectrum_ready = false;
+    // timing
+    bool timing = false;
+    std::vector<hipEvent_t> event_pool;
+    std::vector<TimedLaunch> pending;
+    double kind_ms[3] = {0, 0, 0};
+    long long kind_count[3] = {0, 0, 0};
+
+    size_t texels() const { return (size_t)n * n; }
+    size_t units() const { return (size_t)T * C; }
+
+    ocean::DevView view() const {
+        ocean::DevView v{};
+        v.n = n;
+        v.logn = logn;
+        v.C = C;
+        v.T = T;
+        v.units = T * C;
+        v.planes = P;
+        v.normals = (flags & OCEAN_F_NORMALS) != 0;
+        v.noise = noise;
+        v.h0 = h0;
+        v.waves = waves;
+        for (int p = 0; p < 4; ++p) v.plane[p] = plane[p];
+        v.disp = disp;
+        v.deriv = deriv;
+        v.turb = turb;
+        v.normal = normal;
+        v.tw = tw;
+        v.casc = casc;
+        return v;
+    }
+
+    hipEvent_t take_event() {
+        if (event_pool.empty()) {
+            hipEvent_t e = nullptr;
+            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+            return e;
+        }
+        hipEvent_t e = event_pool.back();
+        event_pool.pop_back();
+        return e;
+    }
+};
+
+namespace {
+
+// Set the device for the calling thread and check the context.
+int enter(ocean_ctx* ctx) {
+    if (!ctx) return fail(OCEAN_E_INVALID_ARG, "null context");
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    return OCEAN_OK;
+}
+
+// Launch wrapper: brackets the launch with events when kernel timing is on.
+template <class F>
+int timed(ocean_ctx* ctx, int kind, F&& launch, const char* what) {
+    hipEvent_t a = nullptr, b = nullptr;
+    if (ctx->timing) {
+        a = ctx->take_event();
+        b = ctx->take_event();
+        if (!a || !b) return fail(OCEAN_E_DEVICE, "hipEventCreate failed");
+        OCEAN_HIP(hipEventRecord(a, ctx->stream));
+    }
+    hipError_t e = launch();
+    if (e != hipSuccess) return hip_fail(e, what);
+    if (ctx->timing) {
+        OCEAN_HIP(hipEventRecord(b, ctx->stream));
+        ctx->pending.push_back({kind, a, b});
+    }
+    return OCEAN_OK;
+}
+
+void* tex_ptr(ocean_ctx* ctx, int tex, size_t* elem_bytes, size_t* slices) {
+    *slices = ctx->units();
+    switch (tex) {
+        case OCEAN_TEX_NOISE: *elem_bytes = 8; *slices = ctx->T; return ctx->noise;
+        case OCEAN_TEX_H0: *elem_bytes = 16; return ctx->h0;
+        case OCEAN_TEX_WAVES: *elem_bytes = 16; return ctx->waves;
+        case OCEAN_TEX_PLANE0:
+        case OCEAN_TEX_PLANE1:
+        case OCEAN_TEX_PLANE2:
+        case OCEAN_TEX_PLANE3: *elem_bytes = 8; return ctx->plane[tex - OCEAN_TEX_PLANE0];
+        case OCEAN_TEX_DISP: *elem_bytes = 16; return ctx->disp;
+        case OCEAN_TEX_DERIV: *elem_bytes = 16; return ctx->deriv;
+        case OCEAN_TEX_TURB: *elem_bytes = 16; return ctx->turb;
+        case OCEAN_TEX_NORMAL: *elem_bytes = 16; return ctx->normal;
+    }
+    return nullptr;
+}
+
+int slice_ptr(ocean_ctx* ctx, int tex, int tile, int cascade, size_t bytes, char** out) {
+    size_t eb = 0, slices = 0;
+    void* base = tex_ptr(ctx, tex, &eb, &slices);
+    if (tex < OCEAN_TEX_NOISE || tex > OCEAN_TEX_NORMAL) return fail(OCEAN_E_INVALID_ARG, "unknown texture id");
+    if (!base) return fail(OCEAN_E_INVALID_ARG, "texture not allocated for this context's flags");
+    if (tile < 0 || tile >= ctx->T) return fail(OCEAN_E_INVALID_ARG, "tile out of range");
+    if (tex != OCEAN_TEX_NOISE && (cascade < 0 || cascade >= ctx->C))
+        return fail(OCEAN_E_INVALID_ARG, "cascade out of range");
+    const size_t slice_bytes = ctx->texels() * eb;
+    if (bytes != slice_bytes)
+        return fail(OCEAN_E_INVALID_ARG, "byte count " + std::to_string(bytes) + " != slice size " +
+                                             std::to_string(slice_bytes));
+    const size_t slice = tex == OCEAN_TEX_NOISE ? (size_t)tile : (size_t)tile * ctx->C + cascade;
+    *out = static_cast<char*>(base) + slice * slice_bytes;
+    return OCEAN_OK;
+}
+
+void free_all(ocean_ctx* c) {
+    void* ptrs[] = {c->noise, c->h0, c->waves, c->plane[0], c->plane[1], c->plane[2], c->plane[3],
+                    c->disp,  c->deriv, c->turb, c->normal, c->tw, c->casc};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    for (auto& t : c->pending) {
+        (void)hipEventDestroy(t.a);
+        (void)hipEventDestroy(t.b);
+    }
+    for (auto e : c->event_pool) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* ocean_last_error(void) { return g_last_error.c_str(); }
+
+int ocean_abi_version(void) { return OCEAN_ABI_VERSION; }
+
+int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags, ocean_ctx** out) {
+    g_last_error.clear();
+    if (!out) return fail(OCEAN_E_INVALID_ARG, "out is null");
+    *out = nullptr;
+    if (n < 16 || n > 4096 || (n & (n - 1)) != 0)
+        return fail(OCEAN_E_UNSUPPORTED, "n must be a power of two in [16, 4096], got " + std::to_string(n));
+    if (n_cascades < 1 || n_cascades > 5)
+        return fail(OCEAN_E_UNSUPPORTED, "n_cascades must be in [1, 5], got " + std::to_string(n_cascades));
+    if (n_tiles < 1) return fail(OCEAN_E_INVALID_ARG, "n_tiles must be >= 1");
+    if (flags & ~(OCEAN_F_DISPLACEMENT_ONLY | OCEAN_F_NORMALS | OCEAN_F_UNFUSED))
+        return fail(OCEAN_E_INVALID_ARG, "unknown flag bits");
+    if ((flags & OCEAN_F_DISPLACEMENT_ONLY) && (flags & OCEAN_F_NORMALS))
+        return fail(OCEAN_E_INVALID_ARG, "NORMALS needs the derivative planes (not DISPLACEMENT_ONLY)");
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
+    if (device < 0 || device >= ndev) return fail(OCEAN_E_INVALID_ARG, "device index out of range");
+    e = hipSetDevice(device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+
+    ocean_ctx* c = new (std::nothrow) ocean_ctx();
+    if (!c) return fail(OCEAN_E_OUT_OF_MEMORY, "host allocation failed");
+    c->device = device;
+    c->n = n;
+    c->logn = 0;
+    while ((1 << c->logn) < n) c->logn++;
+    c->C = n_cascades;
+    c->T = n_tiles;
+    c->flags = flags;
+    c->P = (flags & OCEAN_F_DISPLACEMENT_ONLY) ? 2 : 4;
+    c->noise_set.assign(n_tiles, false);
+
+    auto alloc = [&](void** p, size_t bytes) -> bool {
+        if (hipMalloc(p, bytes) != hipSuccess) return false;
+        return hipMemset(*p, 0, bytes) == hipSuccess;
+    };
+    const size_t tex = c->texels(), U = c->units();
+    bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
+    ok = ok && alloc((void**)&c->noise, tex * c->T * 8);
+    ok = ok && alloc((void**)&c->h0, tex * U * 16);
+    ok = ok && alloc((void**)&c->waves, tex * U * 16);
+    for (int p = 0; p < c->P; ++p) ok = ok && alloc((void**)&c->plane[p], tex * U * 8);
+    ok = ok && alloc((void**)&c->disp, tex * U * 16);
+    if (c->P == 4) {
+        ok = ok && alloc((void**)&c->deriv, tex * U * 16);
+        ok = ok && alloc((void**)&c->turb, tex * U * 16);
+    }
+    if (flags & OCEAN_F_NORMALS) ok = ok && alloc((void**)&c->normal, tex * U * 16);
+    ok = ok && alloc((void**)&c->tw, (size_t)n * 8);
+    ok = ok && alloc((void**)&c->casc, 5 * 4 * 5);
+    if (!ok) {
+        std::string msg = std::string("device allocation failed: ") + hipGetErrorString(hipGetLastError());
+        free_all(c);
+        delete c;
+        return fail(OCEAN_E_OUT_OF_MEMORY, msg);
+    }
+    // twiddle table tw[m] = exp(+2 pi i m / N), double precision then rounded
+    std::vector<float2> tw(n);
+    for (int m = 0; m < n; ++m) {
+        const double a = 2.0 * M_PI * (double)m / (double)n;
+        tw[m] = make_float2((float)std::cos(a), (float)std::sin(a));
+    }
+    e = hipMemcpy(c->tw, tw.data(), (size_t)n * 8, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        free_all(c);
+        delete c;
+        return hip_fail(e, "twiddle upload");
+    }
+    *out = c;
+    return OCEAN_OK;
+}
+
+void ocean_destroy(ocean_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    free_all(ctx);
+    delete ctx;
+}
+
+int ocean_set_params(ocean_ctx* ctx, const ocean_params* params, const ocean_cascade* cascades) {
+    if (int r = enter(ctx)) return r;
+    if (!params || !cascades) return fail(OCEAN_E_INVALID_ARG, "null params/cascades");
+    const ocean_params& p = *params;
+    if (!(p.gravity > 0) || !(p.fetch > 0) || !(p.wind_speed > 0) || !std::isfinite(p.depth))
+        return fail(OCEAN_E_INVALID_ARG, "gravity, fetch and wind_speed must be > 0, depth finite");
+    if (p.wind_dir_x == 0.0f && p.wind_dir_y == 0.0f) return fail(OCEAN_E_INVALID_ARG, "zero wind direction");
+    float h[25];
+    for (int c = 0; c < ctx->C; ++c) {
+        const ocean_cascade& k = cascades[c];
+        if (!(k.wavelength > 0)) return fail(OCEAN_E_INVALID_ARG, "cascade wavelength must be > 0");
+        h[c * 5 + 0] = k.wavelength;
+        h[c * 5 + 1] = k.cutoff_low;
+        h[c * 5 + 2] = k.cutoff_high;
+        h[c * 5 + 3] = k.swell;
+        h[c * 5 + 4] = k.fade;
+    }
+    OCEAN_HIP(hipMemcpyAsync(ctx->casc, h, (size_t)ctx->C * 5 * 4, hipMemcpyHostToDevice, ctx->stream));
+    OCEAN_HIP(hipStreamSynchronize(ctx->stream));
+    ctx->params = {p.wind_speed, p.wind_dir_x, p.wind_dir_y, p.gravity, p.fetch, p.depth};
+    ctx->params_set = true;
+    return OCEAN_OK;
+}
+
+int ocean_set_noise(ocean_ctx* ctx, int tile, const float* rg) {
+    if (int r = enter(ctx)) return r;
+    if (!rg) return fail(OCEAN_E_INVALID_ARG, "null noise");
+    char* dst = nullptr;
+    if (int r = slice_ptr(ctx, OCEAN_TEX_NOISE, tile, 0, ctx->texels() * 8, &dst)) return r;
+    OCEAN_HIP(hipMemcpyAsync(dst, rg, ctx->texels() * 8, hipMemcpyHostToDevice, ctx->stream));
+    OCEAN_HIP(hipStreamSynchronize(ctx->stream));
+    ctx->noise_set[tile] = true;
+    return OCEAN_OK;
+}
+
+int ocean_generate_noise(ocean_ctx* ctx, uint64_t seed) {
+    if (int r = enter(ctx)) return r;
+    std::vector<float> host(ctx->texels() * 2);
+    for (int t = 0; t < ctx->T; ++t) {
+        ocean::generate_noise_host(ctx->n, seed + (uint64_t)t, host.data());
+        if (int r = ocean_set_noise(ctx, t, host.data())) return r;
+    }
+    return OCEAN_OK;
+}
+
+int ocean_init_spectrum(ocean_ctx* ctx) {
+    if (int r = enter(ctx)) return r;
+    if (!ctx->params_set) return fail(OCEAN_E_STATE, "ocean_set_params must precede ocean_init_spectrum");
+    for (int t = 0; t < ctx->T; ++t)
+        if (!ctx->noise_set[t]) return fail(OCEAN_E_STATE, "noise not set for tile " + std::to_string(t));
+    const ocean::DevView v = ctx->view();
+    if (int r = timed(ctx, 2, [&] { return ocean::launch_init_spectrum(v, ctx->params, ctx->stream); },
+                      "init_spectrum"))
+        return r;
+    if (int r = timed(ctx, 2, [&] { return ocean::launch_conjugate(v, ctx->stream); }, "conjugate")) return r;
+    if (ctx->turb) OCEAN_HIP(hipMemsetAsync(ctx->turb, 0, ctx->texels() * ctx->units() * 16, ctx->stream));
+    ctx->spectrum_ready = true;
+    return OCEAN_OK;
+}
+
+int ocean_evolve(ocean_ctx* ctx, float time) {
+    if (int r = enter(ctx)) return r;
+    if (!ctx->spectrum_ready) return fail(OCEAN_E_STATE, "ocean_init_spectrum must precede ocean_evolve");
+    const ocean::DevView v = ctx->view();
+    return timed(ctx, 2, [&] { return ocean::launch_evolve(v, time, ctx->stream); }, "evolve");
+}
+
+int ocean_ifft2d(ocean_ctx* ctx, int plane_mask) {
+    if (int r = enter(ctx)) return r;
+    if (plane_mask < 0 || plane_mask > 15) return fail(OCEAN_E_INVALID_ARG, "plane_mask must be in [0, 15]");
+    const ocean::DevView v = ctx->view();
+    for (int p = 0; p < 4; ++p) {
+        if (!(plane_mask & (1 << p))) continue;
+        if (p >= ctx->P) return fail(OCEAN_E_INVALID_ARG, "plane not allocated (DISPLACEMENT_ONLY context)");
+        if (int r = timed(ctx, 0, [&] { return ocean::launch_ifft_rows(v, p, ctx->stream); }, "ifft_rows")) return r;
+        if (int r = timed(ctx, 1, [&] { return ocean::launch_ifft_cols(v, p, ctx->stream); }, "ifft_cols")) return r;
+    }
+    return OCEAN_OK;
+}
+
+int ocean_fill(ocean_ctx* ctx) {
+    if (int r = enter(ctx)) return r;
+    const ocean::DevView v = ctx->view();
+    return timed(ctx, 2, [&] { return ocean::launch_fill(v, ctx->stream); }, "fill");
+}
+
+int ocean_step(ocean_ctx* ctx, float time) {
+    if (int r = enter(ctx)) return r;
+    if (!ctx->spectrum_ready) return fail(OCEAN_E_STATE, "ocean_init_spectrum must precede ocean_step");
+    if (ctx->flags & OCEAN_F_UNFUSED) {
+        if (int r = ocean_evolve(ctx, time)) return r;
+        if (int r = ocean_ifft2d(ctx, (1 << ctx->P) - 1)) return r;
+        return ocean_fill(ctx);
+    }
+    const ocean::DevView v = ctx->view();
+    if (int r = timed(ctx, 0, [&] { return ocean::launch_pass_a(v, time, ctx->stream); }, "pass_a")) return r;
+    return timed(ctx, 1, [&] { return ocean::launch_pass_b(v, ctx->stream); }, "pass_b");
+}
+
+int ocean_read(ocean_ctx* ctx, int texture, int tile, int cascade, void* dst, size_t bytes) {
+    if (int r = enter(ctx)) return r;
+    if (!dst) return fail(OCEAN_E_INVALID_ARG, "null destination");
+    char* src = nullptr;
+    if (int r = slice_ptr(ctx, texture, tile, cascade, bytes, &src)) return r;
+    OCEAN_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    OCEAN_HIP(hipStreamSynchronize(ctx->stream));
+    return OCEAN_OK;
+}
+
+int ocean_write(ocean_ctx* ctx, int texture, int tile, int cascade, const void* src, size_t bytes) {
+    if (int r = enter(ctx)) return r;
+    if (!src) return fail(OCEAN_E_INVALID_ARG, "null source");
+    char* dst = nullptr;
+    if (int r = slice_ptr(ctx, texture, tile, cascade, bytes, &dst)) return r;
+    OCEAN_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+    OCEAN_HIP(hipStreamSynchronize(ctx->stream));
+    if (texture == OCEAN_TEX_NOISE) ctx->noise_set[tile] = true;
+    return OCEAN_OK;
+}
+
+int ocean_get_device_ptr(ocean_ctx* ctx, int texture, void** ptr, size_t* bytes) {
+    if (!ctx || !ptr || !bytes) return fail(OCEAN_E_INVALID_ARG, "null argument");
+    if (texture < OCEAN_TEX_NOISE || texture > OCEAN_TEX_NORMAL) return fail(OCEAN_E_INVALID_ARG, "unknown texture id");
+    size_t eb = 0, slices = 0;
+    void* base = tex_ptr(ctx, texture, &eb, &slices);
+    if (!base) return fail(OCEAN_E_INVALID_ARG, "texture not allocated for this context's flags");
+    *ptr = base;
+    *bytes = ctx->texels() * eb * slices;
+    return OCEAN_OK;
+}
+
+int ocean_get_stream(ocean_ctx* ctx, void** stream) {
+    if (!ctx || !stream) return fail(OCEAN_E_INVALID_ARG, "null argument");
+    *stream = (void*)ctx->stream;
+    return OCEAN_OK;
+}
+
+int ocean_synchronize(ocean_ctx* ctx) {
+    if (int r = enter(ctx)) return r;
+    OCEAN_HIP(hipStreamSynchronize(ctx->stream));
+    return OCEAN_OK;
+}
+
+int ocean_set_kernel_timing(ocean_ctx* ctx, int enable) {
+    if (int r = enter(ctx)) return r;
+    if (enable && ctx->event_pool.size() < 4096) {
+        // pre-create events so the timed region never creates any
+        while (ctx->event_pool.size() < 4096) {
+            hipEvent_t e = nullptr;
+            OCEAN_HIP(hipEventCreate(&e));
+            ctx->event_pool.push_back(e);
+        }
+    }
+    ctx->timing = enable != 0;
+    return OCEAN_OK;
+}
+
+int ocean_kernel_stats(ocean_ctx* ctx, int kind, double* total_ms, long long* launches) {
+    if (int r = enter(ctx)) return r;
+    if (kind < 0 || kind > 2 || !total_ms || !launches) return fail(OCEAN_E_INVALID_ARG, "bad kind or null output");
+    OCEAN_HIP(hipStreamSynchronize(ctx->stream));
+    for (auto& t : ctx->pending) {
+        float ms = 0.0f;
+        OCEAN_HIP(hipEventElapsedTime(&ms, t.a, t.b));
+        ctx->kind_ms[t.kind] += ms;
+        ctx->kind_count[t.kind] += 1;
+        ctx->event_pool.push_back(t.a);
+        ctx->event_pool.push_back(t.b);
+    }
+    ctx->pending.clear();
+    *total_ms = ctx->kind_ms[kind];
+    *launches = ctx->kind_count[kind];
+    ctx->kind_ms[kind] = 0;
+    ctx->kind_count[kind] = 0;
+    return OCEAN_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,54 @@
+// Internal declarations shared by the C-ABI layer (ocean_abi.cpp) and the HIP
+// kernel translation units (spectrum.hip, fft.hip).  Not part of the ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ocean/ocean.h"
+
+namespace ocean {
+
+// Device-side view of one context: every texture of every (tile, cascade) unit.
+// unit u = tile * C + cascade; each texture is [u][y][x] (see include/ocean/ocean.h).
+struct DevView {
+    int n;       // grid side N
+    int logn;    // log2 N
+    int C;       // cascades
+    int T;       // tiles
+    int units;   // T * C
+    int planes;  // 4 (full) or 2 (displacement only)
+    bool normals;
+    const float2* noise;  // [T][N][N]
+    float4* h0;           // [U][N][N]
+    float4* waves;        // [U][N][N]
+    float2* plane[4];     // [U][N][N] each
+    float4* disp;         // [U][N][N]
+    float4* deriv;        // [U][N][N] (full only)
+    float4* turb;         // [U][N][N] (full only)
+    float4* normal;       // [U][N][N] (normals only)
+    const float2* tw;     // [N] exp(+2 pi i m / N), m < N
+    const float* casc;    // [C][5] wavelength, cutoff_low, cutoff_high, swell, fade (device)
+};
+
+struct SpectrumParams {
+    float wind_speed, wind_dir_x, wind_dir_y, gravity, fetch, depth;
+};
+
+// spectrum.hip
+hipError_t launch_init_spectrum(const DevView& v, const SpectrumParams& p, hipStream_t s);
+hipError_t launch_conjugate(const DevView& v, hipStream_t s);
+hipError_t launch_evolve(const DevView& v, float t, hipStream_t s);
+hipError_t launch_fill(const DevView& v, hipStream_t s);
+
+// fft.hip
+// Standalone operator (IFFT.InverseFastFourierTransform): in-place row pass and
+// column(+permute) pass over plane `p` of every unit.
+hipError_t launch_ifft_rows(const DevView& v, int p, hipStream_t s);
+hipError_t launch_ifft_cols(const DevView& v, int p, hipStream_t s);
+// Fused frame: pass A = evolve + row IFFT of every plane; pass B = column IFFT +
+// permute + fill/foam (+ normals).
+hipError_t launch_pass_a(const DevView& v, float t, hipStream_t s);
+hipError_t launch_pass_b(const DevView& v, hipStream_t s);
+
+}  // namespace ocean

@@ -1,0 +1,178 @@
+// Spectrum kernels for gfx950: initial spectrum (+ Hermitian partner),
+// unfused evolve and unfused fill.  One thread per texel, 16-byte vector loads
+// and stores, grid-strided over every (tile, cascade) unit.
+//
+//   init_spectrum   InitialSpectrum.compute:33-129
+//   conjugate       InitialSpectrum.compute:135-143 (out of place: h0 -> h0)
+//   evolve          TimeDependentSpectrum.compute:20-47
+//   fill            ResultTexturesFiller.compute:16-34
+#include "ocean_internal.h"
+#include "spectrum_math.h"
+
+namespace ocean {
+namespace {
+
+// ---------------- InitialSpectrum.compute helpers (:33-97) -----------------
+struct Sp {
+    float U, g, F, D, wdx, wdy;
+};
+
+__device__ __forceinline__ float angular_frequency(const Sp& p, float k) { return sqrtf(p.g * k); }  // :33-35
+
+__device__ __forceinline__ float tma_correction(const Sp& p, float w) {  // :38-43
+    float wh = w * sqrtf(p.D / p.g);
+    if (wh <= 1.0f) return 0.5f * wh * wh;
+    if (wh < 2.0f) return 1.0f - 0.5f * (2.0f - wh) * (2.0f - wh);
+    return 1.0f;
+}
+
+__device__ __forceinline__ float jonswap(const Sp& p, float w, float wp) {  // :47-56
+    float alpha = 0.076f * powf(fabsf(p.U * p.U / (p.F * p.g)), 0.22f);
+    float gamma = 3.3f;
+    float sigma = w <= wp ? 0.07f : 0.09f;
+    float d = w - wp;
+    float r = expf(-(d * d) / (2.0f * sigma * sigma * wp * wp));
+    return alpha * p.g * p.g / powf(w, 5.0f) * expf(-1.25f * powf(wp / w, 4.0f)) * powf(fabsf(gamma), r);
+}
+
+__device__ __forceinline__ float spread_power(const Sp& p, float w, float wp) {  // :60-66
+    if (w < 1.05f * wp) return 6.97f * powf(fabsf(w / wp), 4.06f);
+    float peak_speed = p.g / wp;
+    float mu = -2.33f - 1.45f * (p.U / peak_speed - 1.17f);
+    return 9.77f * powf(fabsf(w / wp), mu);
+}
+
+__device__ __forceinline__ float normalization_factor(float s) {  // :69-74
+    float s2 = s * s;
+    float s3 = s2 * s;
+    if (s <= 0.4f)
+        return 0.09f * s3 + (powf(logf(2.0f), 2.0f) / kPi - kPi / 12.0f) * s2 + logf(2.0f) / kPi * s +
+               1.0f / (2.0f * kPi);
+    return sqrtf(s) / (2.0f * sqrtf(kPi)) + 1.0f / (16.0f * sqrtf(kPi * s));
+}
+
+__device__ __forceinline__ float directional_spread(const Sp& p, float w, float wp, float theta, float swell) {  // :78-84
+    float s = spread_power(p, w, wp) + 16.0f * tanhf(w / wp) * swell * swell;
+    float len = sqrtf(p.wdx * p.wdx + p.wdy * p.wdy);  // normalize(float2(x, y))
+    float wind_theta = atan2f(p.wdy / len, p.wdx / len);
+    return normalization_factor(s) * powf(fabsf(cosf(0.5f * (theta - wind_theta))), 2.0f * s);
+}
+
+__device__ __forceinline__ float frequency_derivative(const Sp& p, float k, float w) {  // :87-91
+    float th = tanhf(fminf(k * p.D, 20.0f));
+    float ch = coshf(k * p.D);
+    return p.g * (p.D * k / ch / ch + th) / (w * 2.0f);
+}
+
+__device__ __forceinline__ float short_waves_fade(float k, float fade) { return expf(-fade * fade * k * k); }  // :95-97
+
+// CalculateInitialSpectrumTextures (:99-129): one thread per (unit, texel).
+__global__ __launch_bounds__(256) void k_init_spectrum(DevView v, Sp p) {
+    const int n = v.n;
+    const size_t plane = (size_t)n * n;
+    const size_t total = plane * v.units;
+    const float wp = 22.0f * powf(fabsf(p.g * p.g / (p.U * p.F)), 0.3333f);  // :118
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const int u = (int)(i / plane);
+        const size_t t = i - (size_t)u * plane;
+        const int y = (int)(t / n), x = (int)(t - (size_t)y * n);
+        const int tile = u / v.C, c = u - tile * v.C;
+        const float* cs = v.casc + c * 5;
+        const float2 g = v.noise[(size_t)tile * plane + t];
+        const int nx = x - n / 2, nz = y - n / 2;
+        const float dk = 2.0f * kPi / cs[0];  // :110
+        const float kx = (float)nx * dk, kz = (float)nz * dk;
+        const float kmag = sqrtf(kx * kx + kz * kz);
+        float4 h, w;
+        if (kmag >= cs[1] && kmag <= cs[2]) {
+            const float kangle = atan2f(kz, kx);
+            const float om = angular_frequency(p, kmag);
+            const float amp = sqrtf(2.0f * tma_correction(p, om) * jonswap(p, om, wp) *
+                                    directional_spread(p, om, wp, kangle, cs[3]) * short_waves_fade(kmag, cs[4]) *
+                                    frequency_derivative(p, kmag, om) / kmag * dk * dk);
+            h = make_float4(g.x / 2.0f * amp, g.y / 2.0f * amp, 0.0f, 0.0f);
+            w = make_float4(kx, 1.0f / kmag, kz, om);
+        } else {
+            h = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            w = make_float4(kx, 1.0f, kz, 0.0f);
+        }
+        v.h0[i] = h;
+        v.waves[i] = w;
+    }
+}
+
+// CalculateConjugatedInitialSpectrumTextures (:135-143).  h0.xy is never
+// modified by this pass, so reading the mirror's .xy while other threads
+// rewrite their texel is race-free when .xy is written unchanged; we still
+// only store .zw lanes' new values alongside the unchanged .xy.
+__global__ __launch_bounds__(256) void k_conjugate(DevView v) {
+    const int n = v.n;
+    const size_t plane = (size_t)n * n;
+    const size_t total = plane * v.units;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const int u = (int)(i / plane);
+        const size_t t = i - (size_t)u * plane;
+        const int y = (int)(t / n), x = (int)(t - (size_t)y * n);
+        const int mx = (n - x) & (n - 1), my = (n - y) & (n - 1);
+        const float4* src = v.h0 + (size_t)u * plane;
+        const float2 hk = *reinterpret_cast<const float2*>(&src[t]);
+        const float2 hm = *reinterpret_cast<const float2*>(&src[(size_t)my * n + mx]);
+        // write only .zw: .xy stays as is (no writer/reader conflict on .xy)
+        float2* dst = reinterpret_cast<float2*>(&v.h0[i]) + 1;
+        *dst = make_float2(hm.x, -hm.y);
+        (void)hk;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_evolve(DevView v, float time) {
+    const size_t total = (size_t)v.n * v.n * v.units;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        Planes4 o = evolve_texel(v.h0[i], v.waves[i], time);
+        for (int p = 0; p < v.planes; ++p) v.plane[p][i] = o.p[p];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_fill(DevView v) {
+    const size_t total = (size_t)v.n * v.n * v.units;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const float2 a = v.plane[0][i], b = v.plane[1][i];
+        v.disp[i] = make_float4(a.x, b.x, a.y, 1.0f);
+        if (v.planes == 4) {
+            const float2 c = v.plane[2][i], d = v.plane[3][i];
+            v.deriv[i] = make_float4(c.x, c.y, d.x, d.y);
+            const float foam = foam_update(v.turb[i].x, d.x, d.y, b.y);
+            v.turb[i] = make_float4(foam, foam, foam, foam);
+            if (v.normals) v.normal[i] = normal_from_deriv(c.x, c.y, d.x, d.y);
+        }
+    }
+}
+
+unsigned grid_for(size_t total) {
+    size_t g = (total + 255) / 256;
+    return (unsigned)(g < 16384 ? (g == 0 ? 1 : g) : 16384);
+}
+
+}  // namespace
+
+hipError_t launch_init_spectrum(const DevView& v, const SpectrumParams& sp, hipStream_t s) {
+    Sp p{sp.wind_speed, sp.gravity, sp.fetch, sp.depth, sp.wind_dir_x, sp.wind_dir_y};
+    hipLaunchKernelGGL(k_init_spectrum, dim3(grid_for((size_t)v.n * v.n * v.units)), dim3(256), 0, s, v, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_conjugate(const DevView& v, hipStream_t s) {
+    hipLaunchKernelGGL(k_conjugate, dim3(grid_for((size_t)v.n * v.n * v.units)), dim3(256), 0, s, v);
+    return hipGetLastError();
+}
+
+hipError_t launch_evolve(const DevView& v, float t, hipStream_t s) {
+    hipLaunchKernelGGL(k_evolve, dim3(grid_for((size_t)v.n * v.n * v.units)), dim3(256), 0, s, v, t);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill(const DevView& v, hipStream_t s) {
+    hipLaunchKernelGGL(k_fill, dim3(grid_for((size_t)v.n * v.n * v.units)), dim3(256), 0, s, v);
+    return hipGetLastError();
+}
+
+}  // namespace ocean

@@ -1,0 +1,59 @@
+// Per-texel spectrum arithmetic shared by the elementwise kernels (spectrum.hip)
+// and the fused frame kernels (fft.hip).  Every expression keeps the
+// reference's fp32 operation order; the library is built with
+// -ffp-contract=off so no FMA contraction changes a rounding (the phase
+// omega*t at large t is sensitive to one ulp of omega).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace ocean {
+
+constexpr float kPi = 3.14159265f;                         // InitialSpectrum.compute:8
+constexpr float kFoamDecay = 0.135335283236612691894f;     // exp(-2), ResultTexturesFiller.compute:29-30
+
+struct Planes4 {
+    float2 p[4];  // DxDz, DyDxz, DyxDyz, DxxDzz
+};
+
+// TimeDependentSpectrum.compute:20-47 for one texel-cascade.
+__device__ __forceinline__ Planes4 evolve_texel(float4 h, float4 w, float t) {
+    Planes4 o;
+    float phase = w.w * t;
+    float ex = cosf(phase), ey = sinf(phase);
+    // ComplexMult(h0.xy, e) + ComplexMult(h0.zw, conj(e))  (:26)
+    float hx = (h.x * ex - h.y * ey) + (h.z * ex - h.w * (-ey));
+    float hy = (h.x * ey + h.y * ex) + (h.z * (-ey) + h.w * ex);
+    float ihx = -hy, ihy = hx;                                   // :27
+    float ydx_x = ihx * w.x, ydx_y = ihy * w.x;                  // :29
+    float ydz_x = ihx * w.z, ydz_y = ihy * w.z;                  // :30
+    float dx_x = ydx_x * w.y, dx_y = ydx_y * w.y;                // :32
+    float dz_x = ydz_x * w.y, dz_y = ydz_y * w.y;                // :34
+    float aux_x = -hx * w.y, aux_y = -hy * w.y;                  // :36
+    float dxdx_x = aux_x * w.x * w.x, dxdx_y = aux_y * w.x * w.x;  // :38
+    float dzdz_x = aux_x * w.z * w.z, dzdz_y = aux_y * w.z * w.z;  // :39
+    float dzdx_x = aux_x * w.x * w.z, dzdx_y = aux_y * w.x * w.z;  // :40
+    o.p[0] = make_float2(dx_x - dz_y, dx_y + dz_x);              // :42 DxDz
+    o.p[1] = make_float2(hx - dzdx_y, hy + dzdx_x);              // :43 DyDxz
+    o.p[2] = make_float2(ydx_x - ydz_y, ydx_y + ydz_x);          // :44 DyxDyz
+    o.p[3] = make_float2(dxdx_x - dzdz_y, dxdx_y + dzdz_x);      // :45 DxxDzz
+    return o;
+}
+
+// ResultTexturesFiller.compute:27-32: Jacobian and the foam accumulator.
+__device__ __forceinline__ float foam_update(float prev, float dxx, float dzz, float dxz) {
+    float jac = (1.0f + dxx) * (1.0f + dzz) - dxz * dxz;
+    float foam = prev * kFoamDecay;
+    if (foam < jac) foam += jac;
+    return foam;
+}
+
+// Derived per-cascade normal (Water.shader:346-348 applied to one cascade's derivatives).
+__device__ __forceinline__ float4 normal_from_deriv(float dyx, float dyz, float dxx, float dzz) {
+    float sx = dyx / (1.0f + dxx);
+    float sz = dyz / (1.0f + dzz);
+    float inv = 1.0f / sqrtf(sx * sx + 1.0f + sz * sz);
+    return make_float4(-sx * inv, inv, -sz * inv, 0.0f);
+}
+
+}  // namespace ocean

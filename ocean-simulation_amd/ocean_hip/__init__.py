@@ -1,0 +1,352 @@
+"""ocean_hip -- Python host mirror of the reference's WaterBody / IFFT interface
+over liboceanhip.so (the MI355X C ABI declared in include/ocean/ocean.h).
+
+The reference's host side is C# (Unity MonoBehaviours); no C# toolchain exists
+in this image, so the host layer that the tests and the bench drive is this
+ctypes binding, shaped like the reference:
+
+    WaterBody  (Assets/Scripts/Water/WaterBody.cs)  -- fields, Awake(),
+               CalculateWavesTexturesAtTime(t), Update(t), GetWaterHeight(pos)
+    IFFT       (Assets/Scripts/Water/IFFT.cs)       -- InverseFastFourierTransform(plane)
+    WaterCascade (Assets/Scripts/Water/WaterCascade.cs)
+
+A compile-ready C# P/Invoke facade of the same ABI lives in ../csharp/ and in
+INTEGRATION.md.  There is no CPU fallback: if the HIP library cannot be loaded
+(or no GPU is present) every compute call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+# torch is only plumbing here (device count, torch.distributed in bench.py), but
+# its bundled HIP runtime must be the one this library binds to: import it first
+# so that libamdhip64.so.7 resolves to the already-loaded copy (one runtime per
+# process).
+try:  # pragma: no cover - import side effect only
+    import torch as _torch  # noqa: F401
+except Exception:  # torch absent: the library then binds to /opt/rocm's runtime
+    _torch = None
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liboceanhip.so")
+
+OK = 0
+E_INVALID_ARG = -1
+E_UNSUPPORTED = -2
+E_STATE = -3
+E_DEVICE = -4
+E_OUT_OF_MEMORY = -5
+
+F_DISPLACEMENT_ONLY = 0x1
+F_NORMALS = 0x2
+F_UNFUSED = 0x4
+
+TEX_NOISE, TEX_H0, TEX_WAVES = 0, 1, 2
+TEX_PLANE0, TEX_PLANE1, TEX_PLANE2, TEX_PLANE3 = 3, 4, 5, 6
+TEX_DISP, TEX_DERIV, TEX_TURB, TEX_NORMAL = 7, 8, 9, 10
+_TEX_CHANNELS = {TEX_NOISE: 2, TEX_H0: 4, TEX_WAVES: 4, TEX_PLANE0: 2, TEX_PLANE1: 2, TEX_PLANE2: 2,
+                 TEX_PLANE3: 2, TEX_DISP: 4, TEX_DERIV: 4, TEX_TURB: 4, TEX_NORMAL: 4}
+
+# symbols declared in include/ocean/ocean.h
+EXPORTED_SYMBOLS = (
+    "ocean_create", "ocean_destroy", "ocean_set_params", "ocean_set_noise", "ocean_generate_noise",
+    "ocean_init_spectrum", "ocean_step", "ocean_evolve", "ocean_ifft2d", "ocean_fill", "ocean_read",
+    "ocean_write", "ocean_get_device_ptr", "ocean_get_stream", "ocean_synchronize",
+    "ocean_set_kernel_timing", "ocean_kernel_stats", "ocean_last_error", "ocean_abi_version",
+)
+
+
+class OceanError(RuntimeError):
+    def __init__(self, code: int, where: str, msg: str):
+        super().__init__(f"{where} failed ({code}): {msg}")
+        self.code = code
+
+
+class ocean_params(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_float) for n in
+                ("wind_speed", "wind_dir_x", "wind_dir_y", "gravity", "fetch", "depth")]
+
+
+class ocean_cascade(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_float) for n in ("wavelength", "cutoff_low", "cutoff_high", "swell", "fade")]
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load liboceanhip.so (raises if it was not built -- there is no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise OceanError(E_DEVICE, "load_library",
+                         f"{path} not found: build it with `make -C ocean-simulation_amd` "
+                         "(or __graft_entry__.build())")
+    L = ctypes.CDLL(path)
+    P = ctypes.c_void_p
+    i, u32, u64, f, sz = ctypes.c_int, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float, ctypes.c_size_t
+    sig = {
+        "ocean_create": ([i, i, i, i, u32, ctypes.POINTER(P)], i),
+        "ocean_destroy": ([P], None),
+        "ocean_set_params": ([P, ctypes.POINTER(ocean_params), ctypes.POINTER(ocean_cascade)], i),
+        "ocean_set_noise": ([P, i, P], i),
+        "ocean_generate_noise": ([P, u64], i),
+        "ocean_init_spectrum": ([P], i),
+        "ocean_step": ([P, f], i),
+        "ocean_evolve": ([P, f], i),
+        "ocean_ifft2d": ([P, i], i),
+        "ocean_fill": ([P], i),
+        "ocean_read": ([P, i, i, i, P, sz], i),
+        "ocean_write": ([P, i, i, i, P, sz], i),
+        "ocean_get_device_ptr": ([P, i, ctypes.POINTER(P), ctypes.POINTER(sz)], i),
+        "ocean_get_stream": ([P, ctypes.POINTER(P)], i),
+        "ocean_synchronize": ([P], i),
+        "ocean_set_kernel_timing": ([P, i], i),
+        "ocean_kernel_stats": ([P, i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong)], i),
+        "ocean_last_error": ([], ctypes.c_char_p),
+        "ocean_abi_version": ([], i),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = L
+    return L
+
+
+def _check(rc: int, where: str) -> None:
+    if rc != OK:
+        msg = load_library().ocean_last_error().decode(errors="replace")
+        raise OceanError(rc, where, msg)
+
+
+class OceanContext:
+    """Thin owner of one ocean_ctx (one device, T tiles x C cascades at N x N)."""
+
+    def __init__(self, n: int, n_cascades: int, n_tiles: int = 1, flags: int = 0, device: int = 0):
+        self.lib = load_library()
+        self.n, self.C, self.T, self.flags, self.device = n, n_cascades, n_tiles, flags, device
+        self.planes = 2 if flags & F_DISPLACEMENT_ONLY else 4
+        h = ctypes.c_void_p()
+        _check(self.lib.ocean_create(device, n, n_cascades, n_tiles, flags, ctypes.byref(h)), "ocean_create")
+        self._h = h
+
+    # -- lifetime -----------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self.lib.ocean_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # -- configuration --------------------------------------------------------
+    def set_params(self, params: dict, cascades: Sequence[dict]) -> None:
+        if len(cascades) != self.C:
+            raise ValueError(f"expected {self.C} cascades, got {len(cascades)}")
+        p = ocean_params(params["wind_speed"], params["wind_dir_x"], params["wind_dir_y"], params["gravity"],
+                         params["fetch"], params["depth"])
+        cs = (ocean_cascade * self.C)(*[ocean_cascade(c["wavelength"], c["cutoff_low"], c["cutoff_high"],
+                                                      c["swell"], c["fade"]) for c in cascades])
+        _check(self.lib.ocean_set_params(self._h, ctypes.byref(p), cs), "ocean_set_params")
+
+    def set_noise(self, tile: int, rg: np.ndarray) -> None:
+        a = np.ascontiguousarray(rg, np.float32)
+        if a.shape != (self.n, self.n, 2):
+            raise ValueError(f"noise must be float32[{self.n}][{self.n}][2], got {a.shape}")
+        _check(self.lib.ocean_set_noise(self._h, tile, a.ctypes.data), "ocean_set_noise")
+
+    def generate_noise(self, seed: int) -> None:
+        _check(self.lib.ocean_generate_noise(self._h, ctypes.c_uint64(seed)), "ocean_generate_noise")
+
+    # -- compute --------------------------------------------------------------
+    def init_spectrum(self) -> None:
+        _check(self.lib.ocean_init_spectrum(self._h), "ocean_init_spectrum")
+
+    def step(self, t: float) -> None:
+        _check(self.lib.ocean_step(self._h, ctypes.c_float(t)), "ocean_step")
+
+    def evolve(self, t: float) -> None:
+        _check(self.lib.ocean_evolve(self._h, ctypes.c_float(t)), "ocean_evolve")
+
+    def ifft2d(self, plane_mask: int) -> None:
+        _check(self.lib.ocean_ifft2d(self._h, plane_mask), "ocean_ifft2d")
+
+    def fill(self) -> None:
+        _check(self.lib.ocean_fill(self._h), "ocean_fill")
+
+    def synchronize(self) -> None:
+        _check(self.lib.ocean_synchronize(self._h), "ocean_synchronize")
+
+    # -- textures -------------------------------------------------------------
+    def read(self, tex: int, tile: int = 0, cascade: int = 0) -> np.ndarray:
+        ch = _TEX_CHANNELS[tex]
+        out = np.empty((self.n, self.n, ch), np.float32)
+        _check(self.lib.ocean_read(self._h, tex, tile, cascade, out.ctypes.data, out.nbytes), "ocean_read")
+        return out
+
+    def read_all(self, tex: int, tile: int = 0) -> np.ndarray:
+        return np.stack([self.read(tex, tile, c) for c in range(self.C)])
+
+    def write(self, tex: int, data: np.ndarray, tile: int = 0, cascade: int = 0) -> None:
+        a = np.ascontiguousarray(data, np.float32)
+        _check(self.lib.ocean_write(self._h, tex, tile, cascade, a.ctypes.data, a.nbytes), "ocean_write")
+
+    def device_ptr(self, tex: int):
+        p, b = ctypes.c_void_p(), ctypes.c_size_t()
+        _check(self.lib.ocean_get_device_ptr(self._h, tex, ctypes.byref(p), ctypes.byref(b)), "ocean_get_device_ptr")
+        return p.value, b.value
+
+    def stream(self) -> int:
+        s = ctypes.c_void_p()
+        _check(self.lib.ocean_get_stream(self._h, ctypes.byref(s)), "ocean_get_stream")
+        return s.value or 0
+
+    # -- timing ---------------------------------------------------------------
+    def set_kernel_timing(self, enable: bool) -> None:
+        _check(self.lib.ocean_set_kernel_timing(self._h, 1 if enable else 0), "ocean_set_kernel_timing")
+
+    def kernel_stats(self, kind: int):
+        ms, cnt = ctypes.c_double(), ctypes.c_longlong()
+        _check(self.lib.ocean_kernel_stats(self._h, kind, ctypes.byref(ms), ctypes.byref(cnt)), "ocean_kernel_stats")
+        return ms.value, cnt.value
+
+
+# ---------------------------------------------------------------------------
+# Reference-shaped facade
+# ---------------------------------------------------------------------------
+@dataclass
+class WaterCascade:
+    """WaterCascade.cs:10-24 (defaults from the script)."""
+    wavelength: float = 10.0
+    cutoffHigh: float = 5.0
+    cutoffLow: float = 0.0001
+    swell: float = 0.4
+    fade: float = 0.1
+
+    def as_dict(self) -> dict:
+        return dict(wavelength=self.wavelength, cutoff_low=self.cutoffLow, cutoff_high=self.cutoffHigh,
+                    swell=self.swell, fade=self.fade)
+
+
+@dataclass
+class WaterBody:
+    """WaterBody.cs public surface over the HIP library.
+
+    Fields and defaults follow WaterBody.cs:10-33.  Awake() allocates and runs
+    the initial spectrum (WaterBody.cs:211-256); CalculateWavesTexturesAtTime(t)
+    is the per-frame path (WaterBody.cs:180-193); Update(t) additionally reads
+    back displacement slice 0 for GetWaterHeight (WaterBody.cs:284-297, 195-209).
+    `tiles` > 1 batches independent oceans (tile k uses seed + k).
+    """
+    windSpeed: float = 1.0
+    windDirection: tuple = (1.0, 1.0)
+    gravity: float = 9.81
+    fetch: float = 1.0
+    depth: float = 4.0
+    texturesSize: int = 256
+    cascades: List[WaterCascade] = field(default_factory=lambda: [WaterCascade()])
+    seed: int = 20251121
+    tiles: int = 1
+    displacementOnly: bool = False
+    normals: bool = False
+    device: int = 0
+    noise: Optional[np.ndarray] = None  # explicit noise texture (tile 0), float32[N][N][2]
+
+    def __post_init__(self):
+        self.ctx: Optional[OceanContext] = None
+        self.buoyancyData: Optional[np.ndarray] = None
+
+    def params(self) -> dict:
+        return dict(wind_speed=self.windSpeed, wind_dir_x=self.windDirection[0], wind_dir_y=self.windDirection[1],
+                    gravity=self.gravity, fetch=self.fetch, depth=self.depth)
+
+    def Awake(self) -> "WaterBody":
+        flags = (F_DISPLACEMENT_ONLY if self.displacementOnly else 0) | (F_NORMALS if self.normals else 0)
+        self.ctx = OceanContext(self.texturesSize, len(self.cascades), self.tiles, flags, self.device)
+        self.ctx.set_params(self.params(), [c.as_dict() for c in self.cascades])
+        if self.noise is not None:
+            self.ctx.set_noise(0, self.noise)
+            for t in range(1, self.tiles):
+                self.ctx.set_noise(t, self.noise)
+        else:
+            self.ctx.generate_noise(self.seed)
+        self.ctx.init_spectrum()
+        return self
+
+    def OnValidate(self) -> None:
+        """Parameter change -> spectrum re-init (the commented OnValidate, WaterBody.cs:324-337)."""
+        self.ctx.set_params(self.params(), [c.as_dict() for c in self.cascades])
+        self.ctx.init_spectrum()
+
+    def CalculateWavesTexturesAtTime(self, time: float) -> None:
+        self.ctx.step(time)
+
+    def Update(self, time: float) -> None:
+        self.CalculateWavesTexturesAtTime(time)
+        self.buoyancyData = self.ctx.read(TEX_DISP, 0, 0)  # AsyncGPUReadback of slice 0 (synchronous here)
+
+    def GetWaterHeight(self, worldPosition) -> float:
+        """WaterBody.cs:195-209, including its quirk of mapping world x,z over
+        [-texturesSize/2, texturesSize/2] instead of the cascade length."""
+        if self.buoyancyData is None:
+            return 0.0
+        n = self.texturesSize
+
+        def inv_lerp(a, b, v):
+            return 0.0 if a == b else min(max((v - a) / (b - a), 0.0), 1.0)
+        u = inv_lerp(-(n // 2), n // 2, float(worldPosition[0]))
+        v = inv_lerp(-(n // 2), n // 2, float(worldPosition[2]))
+        x = min(max(int(u * n), 0), n - 1)
+        y = min(max(int(v * n), 0), n - 1)
+        return float(self.buoyancyData[y, x, 1])
+
+    # texture-out contract (material properties, WaterBody.cs:277-281)
+    def DisplacementsTextures(self, tile: int = 0) -> np.ndarray:
+        return self.ctx.read_all(TEX_DISP, tile)
+
+    def DerivativesTextures(self, tile: int = 0) -> np.ndarray:
+        return self.ctx.read_all(TEX_DERIV, tile)
+
+    def TurbulenceTextures(self, tile: int = 0) -> np.ndarray:
+        return self.ctx.read_all(TEX_TURB, tile)
+
+    def OnDisable(self) -> None:
+        if self.ctx is not None:
+            self.ctx.close()
+            self.ctx = None
+
+
+class IFFT:
+    """IFFT.cs operator: InverseFastFourierTransform on a plane texture array of a context."""
+
+    def __init__(self, ctx: OceanContext):
+        self.ctx = ctx
+
+    def InverseFastFourierTransform(self, plane: int) -> None:
+        """plane in 0..3 (DxDz, DyDxz, DyxDyz, DxxDzz): in-place, all tiles and cascades."""
+        self.ctx.ifft2d(1 << plane)
+
+
+def scene_water_body(n: int = 512, n_cascades: int = 3, **kw) -> WaterBody:
+    """The reference scene (Assets/Scenes/Waves.unity:1305-1322, cascades :1431-1435, :470-474,
+    :1249-1253, 4th unreferenced cascade :1572-1576)."""
+    cs = [WaterCascade(1530, 1e12, 1e-10, 0.4, 0.1), WaterCascade(1000, 1e7, 1e-7, 0.3, 0.2),
+          WaterCascade(201, 1e6, 1e-5, 0.1, 0.1), WaterCascade(34, 10, 0.001, 0.4, 0.1)][:n_cascades]
+    return WaterBody(windSpeed=8.0, windDirection=(1.0, -1.0), gravity=9.81, fetch=50000.0, depth=2560.0,
+                     texturesSize=n, cascades=cs, **kw)

@@ -1,0 +1,380 @@
+/*
+ * ocean_oracle.c -- CPU restatement of the reference's per-frame ocean path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (the HIP library under
+ * ocean-simulation_amd/) links, loads or calls this file.  It is imported only
+ * by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, as the
+ * checker / CPU baseline, never as the thing measured or shipped.
+ *
+ * What it follows (reference = Mozobo/Ocean-Simulation @ 2025-11-21):
+ *   noise           Assets/Scripts/Water/WaterBody.cs:71-100  (Marsaglia polar,
+ *                   x-outer / y-inner, g1 then g2).  Unity's RNG is closed
+ *                   source and unseeded, so the uniform source is this
+ *                   project's own documented xorshift128 (see noise section).
+ *   init spectrum   Assets/Shaders/Compute Shaders/Water/InitialSpectrum.compute:33-129
+ *   conjugate       InitialSpectrum.compute:135-143
+ *   evolve          TimeDependentSpectrum.compute:16-47
+ *   IFFT            IFFT.compute:21-78 driven by Assets/Scripts/Water/IFFT.cs:24-94
+ *                   (twiddle/index table, log2N horizontal + log2N vertical
+ *                   radix-2 ping-pong passes, then the (-1)^(x+y) permute)
+ *   fill / foam     ResultTexturesFiller.compute:16-34
+ *   frame schedule  WaterBody.cs:180-193
+ *
+ * All arithmetic is IEEE fp32 in the reference's operation order (compile with
+ * -ffp-contract=off so no FMA contraction changes roundings).  Transcendentals
+ * come from glibc's libm (the reference uses the GPU vendor's HLSL intrinsics;
+ * that difference is covered by the stated tolerance).
+ *
+ * Parity status: the reference ships no tests, fixtures or golden vectors and
+ * cannot be built or run here (Unity + HLSL, no C# toolchain).
+ * This restatement is therefore "parity unpinned" by reference-produced
+ * vectors; it is cross-checked instead by independent known-answer tests
+ * (numpy.fft identity, analytic plane wave, foam recurrence, Hermitian
+ * symmetry) and an fp64 numpy restatement -- see tests/test_oracle.py.
+ *
+ * Layouts (match the reference's Texture2DArray indexing [slice][y][x]):
+ *   noise   float2 [N][N]          texel (x, y) at (y*N + x)*2
+ *   h0      float4 [C][N][N]
+ *   waves   float4 [C][N][N]       (kx, 1/|k|, kz, omega)
+ *   plane   float2 [C][N][N]       one of DxDz, DyDxz, DyxDyz, DxxDzz
+ *   disp    float4 [C][N][N]       (Dx, Dy, Dz, 1)   (alpha unspecified in reference)
+ *   deriv   float4 [C][N][N]       (Dyx, Dyz, Dxx, Dzz)
+ *   turb    float4 [C][N][N]       (foam, foam, foam, foam)
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define OR_PI 3.14159265f /* InitialSpectrum.compute:8, IFFT.compute:7 */
+
+typedef struct {
+    float wind_speed, wind_dir_x, wind_dir_y, gravity, fetch, depth;
+} or_params;
+
+typedef struct {
+    float wavelength, cutoff_low, cutoff_high, swell, fade;
+} or_cascade;
+
+/* ------------------------------------------------------------------------ */
+/* Noise: WaterBody.cs:71-100.  Uniform source: xorshift128 (Marsaglia 2003)  */
+/* seeded by splitmix64(seed); U = (u32 >> 8) * 2^-24 in [0, 1).             */
+/* ------------------------------------------------------------------------ */
+typedef struct { uint32_t s[4]; } or_rng;
+
+static uint64_t or_splitmix64(uint64_t *x) {
+    uint64_t z = (*x += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+static void or_rng_seed(or_rng *r, uint64_t seed) {
+    uint64_t x = seed;
+    uint64_t a = or_splitmix64(&x), b = or_splitmix64(&x);
+    r->s[0] = (uint32_t)a; r->s[1] = (uint32_t)(a >> 32);
+    r->s[2] = (uint32_t)b; r->s[3] = (uint32_t)(b >> 32);
+    if ((r->s[0] | r->s[1] | r->s[2] | r->s[3]) == 0) r->s[0] = 1u;
+}
+
+static uint32_t or_rng_next(or_rng *r) {
+    uint32_t t = r->s[0] ^ (r->s[0] << 11);
+    r->s[0] = r->s[1]; r->s[1] = r->s[2]; r->s[2] = r->s[3];
+    r->s[3] = r->s[3] ^ (r->s[3] >> 19) ^ t ^ (t >> 8);
+    return r->s[3];
+}
+
+static float or_uniform(or_rng *r) { return (float)(or_rng_next(r) >> 8) * (1.0f / 16777216.0f); }
+
+/* WaterBody.cs:71-81 GenerateRandomNumber */
+static float or_gaussian(or_rng *r) {
+    float v1, v2, s;
+    do {
+        v1 = 2.0f * or_uniform(r) - 1.0f;
+        v2 = 2.0f * or_uniform(r) - 1.0f;
+        s = v1 * v1 + v2 * v2;
+    } while (s >= 1.0f || s == 0.0f);
+    s = sqrtf((-2.0f * logf(s)) / s);
+    return v1 * s;
+}
+
+/* WaterBody.cs:86-100: i (=x) outer, j (=y) inner; SetPixel(i, j, (g1, g2)). */
+void oracle_generate_noise(int n, uint64_t seed, float *noise) {
+    or_rng r;
+    or_rng_seed(&r, seed);
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) {
+            float g1 = or_gaussian(&r);
+            float g2 = or_gaussian(&r);
+            noise[((size_t)j * n + i) * 2 + 0] = g1;
+            noise[((size_t)j * n + i) * 2 + 1] = g2;
+        }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Initial spectrum: InitialSpectrum.compute:33-129                          */
+/* ------------------------------------------------------------------------ */
+static float or_angular_frequency(const or_params *p, float k) { /* :33-35 */
+    return sqrtf(p->gravity * k);
+}
+
+static float or_tma(const or_params *p, float w) { /* :38-43 */
+    float wh = w * sqrtf(p->depth / p->gravity);
+    if (wh <= 1.0f) return 0.5f * wh * wh;
+    if (wh < 2.0f) return 1.0f - 0.5f * (2.0f - wh) * (2.0f - wh);
+    return 1.0f;
+}
+
+static float or_jonswap(const or_params *p, float w, float wp) { /* :47-56 */
+    float alpha = 0.076f * powf(fabsf(p->wind_speed * p->wind_speed / (p->fetch * p->gravity)), 0.22f);
+    float gamma = 3.3f;
+    float sigma = w <= wp ? 0.07f : 0.09f;
+    float d = w - wp;
+    float r = expf(-(d * d) / (2.0f * sigma * sigma * wp * wp));
+    return alpha * p->gravity * p->gravity / powf(w, 5.0f) * expf(-1.25f * powf(wp / w, 4.0f)) *
+           powf(fabsf(gamma), r);
+}
+
+static float or_spread_power(const or_params *p, float w, float wp) { /* :60-66 */
+    if (w < 1.05f * wp) return 6.97f * powf(fabsf(w / wp), 4.06f);
+    float peak_speed = p->gravity / wp;
+    float mu = -2.33f - 1.45f * (p->wind_speed / peak_speed - 1.17f);
+    return 9.77f * powf(fabsf(w / wp), mu);
+}
+
+static float or_normalization(float s) { /* :69-74 */
+    float s2 = s * s;
+    float s3 = s2 * s;
+    if (s <= 0.4f)
+        return 0.09f * s3 + (powf(logf(2.0f), 2.0f) / OR_PI - OR_PI / 12.0f) * s2 + logf(2.0f) / OR_PI * s +
+               1.0f / (2.0f * OR_PI);
+    return sqrtf(s) / (2.0f * sqrtf(OR_PI)) + 1.0f / (16.0f * sqrtf(OR_PI * s));
+}
+
+static float or_directional_spread(const or_params *p, float w, float wp, float theta, float swell) { /* :78-84 */
+    float s = or_spread_power(p, w, wp) + 16.0f * tanhf(w / wp) * swell * swell;
+    /* normalize(float2(x, y)): v / |v| */
+    float len = sqrtf(p->wind_dir_x * p->wind_dir_x + p->wind_dir_y * p->wind_dir_y);
+    float nx = p->wind_dir_x / len, ny = p->wind_dir_y / len;
+    float wind_theta = atan2f(ny, nx);
+    return or_normalization(s) * powf(fabsf(cosf(0.5f * (theta - wind_theta))), 2.0f * s);
+}
+
+static float or_frequency_derivative(const or_params *p, float k, float w) { /* :87-91 */
+    float th = tanhf(fminf(k * p->depth, 20.0f));
+    float ch = coshf(k * p->depth);
+    return p->gravity * (p->depth * k / ch / ch + th) / (w * 2.0f);
+}
+
+static float or_short_waves_fade(float k, float fade) { /* :95-97 */
+    return expf(-fade * fade * k * k);
+}
+
+/* CalculateInitialSpectrumTextures (:99-129) for all C cascades.
+ * h0/waves: float4[C][N][N].  h0.zw = 0 after this pass. */
+void oracle_init_spectrum(int n, int ncasc, const or_params *p, const or_cascade *cs, const float *noise, float *h0,
+                          float *waves) {
+    int half = n / 2;
+    float wp = 22.0f * powf(fabsf(p->gravity * p->gravity / (p->wind_speed * p->fetch)), 0.3333f); /* :118 */
+    for (int c = 0; c < ncasc; c++) {
+        float dk = 2.0f * OR_PI / cs[c].wavelength; /* :110 */
+        for (int y = 0; y < n; y++)
+            for (int x = 0; x < n; x++) {
+                size_t t = (size_t)y * n + x;
+                size_t o = (((size_t)c * n + y) * n + x) * 4;
+                int nx = x - half, nz = y - half;
+                float g1 = noise[t * 2 + 0], g2 = noise[t * 2 + 1];
+                float kx = (float)nx * dk, kz = (float)nz * dk;
+                float kmag = sqrtf(kx * kx + kz * kz);
+                if (kmag >= cs[c].cutoff_low && kmag <= cs[c].cutoff_high) {
+                    float kangle = atan2f(kz, kx);
+                    float w = or_angular_frequency(p, kmag);
+                    float amp = sqrtf(2.0f * or_tma(p, w) * or_jonswap(p, w, wp) *
+                                      or_directional_spread(p, w, wp, kangle, cs[c].swell) *
+                                      or_short_waves_fade(kmag, cs[c].fade) * or_frequency_derivative(p, kmag, w) /
+                                      kmag * dk * dk);
+                    h0[o + 0] = g1 / 2.0f * amp;
+                    h0[o + 1] = g2 / 2.0f * amp;
+                    h0[o + 2] = 0.0f;
+                    h0[o + 3] = 0.0f;
+                    waves[o + 0] = kx;
+                    waves[o + 1] = 1.0f / kmag;
+                    waves[o + 2] = kz;
+                    waves[o + 3] = w;
+                } else {
+                    h0[o + 0] = h0[o + 1] = h0[o + 2] = h0[o + 3] = 0.0f;
+                    waves[o + 0] = kx;
+                    waves[o + 1] = 1.0f;
+                    waves[o + 2] = kz;
+                    waves[o + 3] = 0.0f;
+                }
+            }
+    }
+}
+
+/* CalculateConjugatedInitialSpectrumTextures (:135-143), written out of place
+ * from the .xy values (the reference's in-place race only ever reads .xy,
+ * which no thread changes, so out-of-place is equivalent). */
+void oracle_conjugate_spectrum(int n, int ncasc, float *h0) {
+    size_t plane = (size_t)n * n;
+    float *xy = (float *)malloc(plane * 2 * sizeof(float));
+    for (int c = 0; c < ncasc; c++) {
+        float *h = h0 + (size_t)c * plane * 4;
+        for (size_t t = 0; t < plane; t++) { xy[t * 2] = h[t * 4]; xy[t * 2 + 1] = h[t * 4 + 1]; }
+        for (int y = 0; y < n; y++)
+            for (int x = 0; x < n; x++) {
+                int mx = (n - x) % n, my = (n - y) % n;
+                size_t t = (size_t)y * n + x, m = (size_t)my * n + mx;
+                h[t * 4 + 0] = xy[t * 2 + 0];
+                h[t * 4 + 1] = xy[t * 2 + 1];
+                h[t * 4 + 2] = xy[m * 2 + 0];
+                h[t * 4 + 3] = -xy[m * 2 + 1];
+            }
+    }
+    free(xy);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Time-dependent spectrum: TimeDependentSpectrum.compute:16-47              */
+/* planes[4]: each float2[C][N][N]: DxDz, DyDxz, DyxDyz, DxxDzz (:42-45).     */
+/* ------------------------------------------------------------------------ */
+void oracle_evolve(int n, int ncasc, const float *h0, const float *waves, float t, float *p0, float *p1, float *p2,
+                   float *p3) {
+    size_t cnt = (size_t)ncasc * n * n;
+    for (size_t i = 0; i < cnt; i++) {
+        const float *w = waves + i * 4;
+        const float *h = h0 + i * 4;
+        float phase = w[3] * t;
+        float ex = cosf(phase), ey = sinf(phase);
+        /* ComplexMult(h0.xy, e) + ComplexMult(h0.zw, conj(e)) */
+        float hx = (h[0] * ex - h[1] * ey) + (h[2] * ex - h[3] * (-ey));
+        float hy = (h[0] * ey + h[1] * ex) + (h[2] * (-ey) + h[3] * ex);
+        float ihx = -hy, ihy = hx;
+        float ydx_x = ihx * w[0], ydx_y = ihy * w[0];
+        float ydz_x = ihx * w[2], ydz_y = ihy * w[2];
+        float dx_x = ydx_x * w[1], dx_y = ydx_y * w[1];
+        float dy_x = hx, dy_y = hy;
+        float dz_x = ydz_x * w[1], dz_y = ydz_y * w[1];
+        float aux_x = -hx * w[1], aux_y = -hy * w[1];
+        float dxdx_x = aux_x * w[0] * w[0], dxdx_y = aux_y * w[0] * w[0];
+        float dzdz_x = aux_x * w[2] * w[2], dzdz_y = aux_y * w[2] * w[2];
+        float dzdx_x = aux_x * w[0] * w[2], dzdx_y = aux_y * w[0] * w[2];
+        p0[i * 2 + 0] = dx_x - dz_y;     p0[i * 2 + 1] = dx_y + dz_x;
+        p1[i * 2 + 0] = dy_x - dzdx_y;   p1[i * 2 + 1] = dy_y + dzdx_x;
+        p2[i * 2 + 0] = ydx_x - ydz_y;   p2[i * 2 + 1] = ydx_y + ydz_x;
+        p3[i * 2 + 0] = dxdx_x - dzdz_y; p3[i * 2 + 1] = dxdx_y + dzdz_x;
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* IFFT: IFFT.compute:37-78 + IFFT.cs:24-94                                  */
+/* ------------------------------------------------------------------------ */
+static int or_log2(int n) { int l = 0; while ((1 << l) < n) l++; return l; }
+
+/* PrecomputeTwiddleFactorsAndInputIndices (:37-45) -> table float4[log2N][N] */
+void oracle_twiddle_table(int n, float *table) {
+    int logn = or_log2(n);
+    float mult_y = 2.0f * OR_PI * 1.0f / (float)n; /* (2*PI*float2(0,1)/N).y */
+    for (int s = 0; s < logn; s++)
+        for (int y = 0; y < n / 2; y++) {
+            unsigned b = (unsigned)n >> (s + 1);
+            unsigned i = (2u * b * (y / b) + y % b) % (unsigned)n;
+            float arg = -mult_y * (float)((y / b) * b); /* ComplexExp(-mult * j): exp(-0)=1 */
+            float tx = cosf(arg), ty = sinf(arg);
+            float *a = table + ((size_t)s * n + y) * 4;
+            float *bb = table + ((size_t)s * n + y + n / 2) * 4;
+            a[0] = tx;  a[1] = ty;  a[2] = (float)i; a[3] = (float)(i + b);
+            bb[0] = -tx; bb[1] = -ty; bb[2] = (float)i; bb[3] = (float)(i + b);
+        }
+}
+
+/* InverseFastFourierTransform (IFFT.cs:66-94) on one float2[C][N][N] plane
+ * array, in place; `pingpong` is caller scratch of the same size. */
+void oracle_ifft2d(int n, int ncasc, const float *table, float *input, float *pingpong) {
+    int logn = or_log2(n);
+    int pp = 0;
+    for (int dir = 0; dir < 2; dir++) {
+        for (int s = 0; s < logn; s++) {
+            const float *src = pp ? pingpong : input;
+            float *dst = pp ? input : pingpong;
+            for (int c = 0; c < ncasc; c++)
+                for (int y = 0; y < n; y++)
+                    for (int x = 0; x < n; x++) {
+                        /* Horizontal (:48-57) indexes the table by x, Vertical (:60-69) by y */
+                        const float *d = table + ((size_t)s * n + (dir == 0 ? x : y)) * 4;
+                        float wx = d[0], wy = -d[1];
+                        unsigned i0 = (unsigned)d[2], i1 = (unsigned)d[3];
+                        size_t a0, a1;
+                        if (dir == 0) {
+                            a0 = ((size_t)c * n + y) * n + i0;
+                            a1 = ((size_t)c * n + y) * n + i1;
+                        } else {
+                            a0 = ((size_t)c * n + i0) * n + x;
+                            a1 = ((size_t)c * n + i1) * n + x;
+                        }
+                        float bx = src[a1 * 2], by = src[a1 * 2 + 1];
+                        size_t o = (((size_t)c * n + y) * n + x) * 2;
+                        dst[o + 0] = src[a0 * 2 + 0] + (wx * bx - wy * by);
+                        dst[o + 1] = src[a0 * 2 + 1] + (wx * by + wy * bx);
+                    }
+            pp = !pp;
+        }
+    }
+    /* 2*log2N passes: even, so the result is back in `input`. Permute (:73-78). */
+    for (int c = 0; c < ncasc; c++)
+        for (int y = 0; y < n; y++)
+            for (int x = 0; x < n; x++) {
+                float sgn = 1.0f - 2.0f * (float)((x + y) % 2);
+                size_t o = (((size_t)c * n + y) * n + x) * 2;
+                input[o] *= sgn;
+                input[o + 1] *= sgn;
+            }
+}
+
+/* ------------------------------------------------------------------------ */
+/* FillResultTextures: ResultTexturesFiller.compute:16-34                    */
+/* ------------------------------------------------------------------------ */
+#define OR_FOAM_DECAY 0.135335283236612691894f /* exp(-2), :29-30 */
+
+void oracle_fill(int n, int ncasc, const float *p0, const float *p1, const float *p2, const float *p3, float *disp,
+                 float *deriv, float *turb) {
+    size_t cnt = (size_t)ncasc * n * n;
+    for (size_t i = 0; i < cnt; i++) {
+        disp[i * 4 + 0] = p0[i * 2 + 0];
+        disp[i * 4 + 1] = p1[i * 2 + 0];
+        disp[i * 4 + 2] = p0[i * 2 + 1];
+        disp[i * 4 + 3] = 1.0f;
+        if (deriv) {
+            deriv[i * 4 + 0] = p2[i * 2 + 0];
+            deriv[i * 4 + 1] = p2[i * 2 + 1];
+            deriv[i * 4 + 2] = p3[i * 2 + 0];
+            deriv[i * 4 + 3] = p3[i * 2 + 1];
+        }
+        if (turb) {
+            float jac = (1.0f + p3[i * 2 + 0]) * (1.0f + p3[i * 2 + 1]) - p1[i * 2 + 1] * p1[i * 2 + 1];
+            float foam = turb[i * 4 + 0];
+            foam *= OR_FOAM_DECAY;
+            if (foam < jac) foam += jac;
+            turb[i * 4 + 0] = turb[i * 4 + 1] = turb[i * 4 + 2] = turb[i * 4 + 3] = foam;
+        }
+    }
+}
+
+/* CalculateWavesTexturesAtTime (WaterBody.cs:180-193) minus GenerateMips.
+ * planes: 4 * C*N*N float2 (scratch/outputs), pingpong: C*N*N float2.
+ * nplanes = 4 (full) or 2 (displacement only: DxDz, DyDxz; deriv/turb NULL). */
+void oracle_step(int n, int ncasc, int nplanes, const float *h0, const float *waves, const float *table, float t,
+                 float *planes, float *pingpong, float *disp, float *deriv, float *turb) {
+    size_t psz = (size_t)ncasc * n * n * 2;
+    float *p[4] = {planes, planes + psz, planes + 2 * psz, planes + 3 * psz};
+    if (nplanes == 4) {
+        oracle_evolve(n, ncasc, h0, waves, t, p[0], p[1], p[2], p[3]);
+    } else {
+        float *tmp = (float *)malloc(psz * 2 * sizeof(float));
+        oracle_evolve(n, ncasc, h0, waves, t, p[0], p[1], tmp, tmp + psz);
+        free(tmp);
+    }
+    for (int i = 0; i < nplanes; i++) oracle_ifft2d(n, ncasc, table, p[i], pingpong);
+    oracle_fill(n, ncasc, p[0], p[1], nplanes == 4 ? p[2] : NULL, nplanes == 4 ? p[3] : NULL, disp,
+                nplanes == 4 ? deriv : NULL, nplanes == 4 ? turb : NULL);
+}

@@ -1,0 +1,89 @@
+"""CPU tests of the C-ABI boundary (no compute calls: no GPU here).
+
+- liboceanhip.so loads and exports every symbol declared in include/ocean/ocean.h
+- argument validation that happens before any device call
+- the Python host mirror's surface matches the reference's (WaterBody / IFFT / WaterCascade)
+"""
+import os
+import re
+import subprocess
+
+import pytest
+
+import ocean_hip as oh
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "ocean", "ocean.h")
+
+
+def header_symbols():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(ocean_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_built_for_gfx950():
+    lib = oh.LIB_PATH
+    assert os.path.exists(lib), "run __graft_entry__.build() first"
+    data = open(lib, "rb").read()
+    assert b"gfx950" in data
+    assert b"__CLANG_OFFLOAD_BUNDLE__" in data
+
+
+def test_exports_every_header_symbol():
+    L = oh.load_library()
+    syms = header_symbols()
+    assert len(syms) >= 19
+    for s in syms:
+        assert hasattr(L, s), f"{s} declared in ocean.h but not exported"
+    assert set(syms) == set(oh.EXPORTED_SYMBOLS)
+    # and nothing else with C linkage under the ocean_ prefix
+    out = subprocess.check_output(["nm", "-D", "--defined-only", oh.LIB_PATH]).decode()
+    exported = sorted({ln.split()[-1] for ln in out.splitlines() if re.search(r" T ocean_", ln)})
+    assert exported == syms
+
+
+def test_abi_version():
+    assert oh.load_library().ocean_abi_version() == 1
+
+
+@pytest.mark.parametrize("n,c,t,code", [(100, 1, 1, oh.E_UNSUPPORTED), (8, 1, 1, oh.E_UNSUPPORTED),
+                                         (8192, 1, 1, oh.E_UNSUPPORTED), (64, 0, 1, oh.E_UNSUPPORTED),
+                                         (64, 6, 1, oh.E_UNSUPPORTED), (64, 1, 0, oh.E_INVALID_ARG)])
+def test_create_validates_before_touching_device(n, c, t, code):
+    with pytest.raises(oh.OceanError) as ei:
+        oh.OceanContext(n, c, t)
+    assert ei.value.code == code
+    assert oh.load_library().ocean_last_error()
+
+
+def test_create_rejects_bad_flags():
+    with pytest.raises(oh.OceanError) as ei:
+        oh.OceanContext(64, 1, 1, flags=0x80)
+    assert ei.value.code == oh.E_INVALID_ARG
+    with pytest.raises(oh.OceanError) as ei:
+        oh.OceanContext(64, 1, 1, flags=oh.F_DISPLACEMENT_ONLY | oh.F_NORMALS)
+    assert ei.value.code == oh.E_INVALID_ARG
+
+
+def test_null_context_is_an_error_not_a_crash():
+    import ctypes
+    L = oh.load_library()
+    assert L.ocean_step(None, ctypes.c_float(0.0)) == oh.E_INVALID_ARG
+    assert L.ocean_synchronize(None) == oh.E_INVALID_ARG
+    L.ocean_destroy(None)  # no-op
+
+
+def test_host_mirror_surface_matches_reference():
+    """WaterBody.cs public fields/methods and defaults (WaterBody.cs:10-33, 180, 195)."""
+    wb = oh.WaterBody()
+    assert (wb.windSpeed, wb.windDirection, wb.gravity, wb.fetch, wb.depth, wb.texturesSize) == \
+        (1.0, (1.0, 1.0), 9.81, 1.0, 4.0, 256)
+    for name in ("Awake", "CalculateWavesTexturesAtTime", "Update", "GetWaterHeight", "OnDisable", "OnValidate"):
+        assert callable(getattr(wb, name))
+    assert wb.GetWaterHeight((0.0, 0.0, 0.0)) == 0.0  # no readback yet -> 0 (WaterBody.cs:197)
+    c = oh.WaterCascade()
+    assert (c.wavelength, c.cutoffHigh, c.cutoffLow, c.swell, c.fade) == (10.0, 5.0, 0.0001, 0.4, 0.1)
+    scene = oh.scene_water_body()
+    assert scene.texturesSize == 512 and len(scene.cascades) == 3 and scene.windDirection == (1.0, -1.0)
+    assert callable(oh.IFFT.InverseFastFourierTransform)

@@ -1,0 +1,332 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the CPU oracle.
+
+Tolerance: every output channel of every cascade within
+norm-relative error max|gpu - oracle| / max|oracle| <= 1e-5 (north_star: "fp32
+outputs within 1e-5 relative"); integer-exact quantities (noise, wave numbers,
+omega) bit-exact.  Run with `python -m pytest tests -m gpu` on an MI355X.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import ocean_hip as oh
+import oracle as O
+
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("require_gpu")]
+
+TOL = 1e-5
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def cplx(a):
+    return a[..., 0].astype(np.float64) + 1j * a[..., 1].astype(np.float64)
+
+
+def make_ctx(n, cascades, params=None, tiles=1, flags=0, seeds=None):
+    ctx = oh.OceanContext(n, len(cascades), tiles, flags)
+    ctx.set_params(params or O.scene_params(), cascades)
+    noises = []
+    for t in range(tiles):
+        nz = O.generate_noise(n, (seeds or [20251121 + k for k in range(tiles)])[t])
+        ctx.set_noise(t, nz)
+        noises.append(nz)
+    ctx.init_spectrum()
+    return ctx, noises
+
+
+def assert_channels(gpu, ref, tol=TOL, what=""):
+    """gpu/ref [C][N][N][ch]: norm-relative error per cascade per channel."""
+    for c in range(ref.shape[0]):
+        for ch in range(ref.shape[-1]):
+            e = O.rel_err(gpu[c, ..., ch], ref[c, ..., ch])
+            assert e <= tol, f"{what} cascade {c} channel {ch}: rel err {e:.3e} > {tol}"
+
+
+# ------------------------------------------------------------------ init
+def test_generated_noise_bit_exact():
+    ctx = oh.OceanContext(64, 1, 3)
+    ctx.generate_noise(777)
+    for t in range(3):
+        np.testing.assert_array_equal(ctx.read(oh.TEX_NOISE, t), O.generate_noise(64, 777 + t))
+    ctx.close()
+
+
+@pytest.mark.parametrize("shallow", [False, True])
+@pytest.mark.parametrize("n", [16, 128, 512])
+def test_init_spectrum(n, shallow):
+    ctx, (noise,) = make_ctx(n, O.SCENE_CASCADES, O.scene_params(shallow))
+    h0, waves = O.init_spectrum(n, O.scene_params(shallow), O.SCENE_CASCADES, noise)
+    g_h0, g_w = ctx.read_all(oh.TEX_H0), ctx.read_all(oh.TEX_WAVES)
+    # kx, kz, 1/|k| and omega use only correctly rounded + - * / sqrt: bit-exact
+    np.testing.assert_array_equal(g_w, waves)
+    assert_channels(g_h0, h0, what="h0")
+    ctx.close()
+
+
+# ------------------------------------------------------------ operators
+@pytest.mark.parametrize("t", [0.0, 1.25, 100.0])
+def test_evolve_operator(t):
+    n = 64
+    ctx, (noise,) = make_ctx(n, O.SCENE_CASCADES)
+    h0, waves = O.init_spectrum(n, O.scene_params(), O.SCENE_CASCADES, noise)
+    ctx.evolve(t)
+    ref = O.evolve(h0, waves, t)
+    for p in range(4):
+        got = ctx.read_all(oh.TEX_PLANE0 + p)
+        assert_channels(got, ref[p], tol=2e-6, what=f"plane {p}")
+    ctx.close()
+
+
+@pytest.mark.parametrize("n", [16, 32, 64, 128, 256, 512, 1024])
+def test_ifft2d_operator_vs_oracle(n):
+    """IFFT.InverseFastFourierTransform on random planes vs the reference's radix-2 schedule."""
+    C = 2
+    ctx = oh.OceanContext(n, C, 1)
+    rng = np.random.default_rng(n)
+    planes = [rng.standard_normal((C, n, n, 2)).astype(np.float32) for _ in range(4)]
+    for p in range(4):
+        for c in range(C):
+            ctx.write(oh.TEX_PLANE0 + p, planes[p][c], 0, c)
+    oh.IFFT(ctx).InverseFastFourierTransform(2)   # plane 2 only
+    ctx.ifft2d(0b1001)                             # planes 0 and 3
+    for p in range(4):
+        got = ctx.read_all(oh.TEX_PLANE0 + p)
+        if p == 1:
+            np.testing.assert_array_equal(got, planes[p])  # untouched
+            continue
+        want = O.ifft2d(planes[p])
+        assert O.rel_err(cplx(got), cplx(want)) <= TOL
+        assert O.rel_err(cplx(got), O.ref64.ifft2d(cplx(planes[p]))) <= 2e-6
+    ctx.close()
+
+
+@pytest.mark.parametrize("n", [2048, 4096])
+def test_ifft2d_operator_large_vs_numpy(n):
+    ctx = oh.OceanContext(n, 1, 1)
+    rng = np.random.default_rng(1)
+    x = rng.standard_normal((1, n, n, 2)).astype(np.float32)
+    ctx.write(oh.TEX_PLANE0, x[0])
+    ctx.ifft2d(1)
+    got = cplx(ctx.read_all(oh.TEX_PLANE0))
+    assert O.rel_err(got, O.ref64.ifft2d(cplx(x))) <= 2e-6
+    ctx.close()
+
+
+def test_ifft2d_delta_and_linearity_at_1024():
+    """Size-independent properties at the bench size: delta -> plane wave; linearity."""
+    n = 1024
+    ctx = oh.OceanContext(n, 1, 1)
+    d = np.zeros((n, n, 2), np.float32)
+    d[7, 300, 0] = 1.0
+    ctx.write(oh.TEX_PLANE0, d)
+    rng = np.random.default_rng(5)
+    a = rng.standard_normal((n, n, 2)).astype(np.float32)
+    b = rng.standard_normal((n, n, 2)).astype(np.float32)
+    ctx.write(oh.TEX_PLANE1, a)
+    ctx.write(oh.TEX_PLANE2, b)
+    ctx.write(oh.TEX_PLANE3, (2 * a - b).astype(np.float32))
+    ctx.ifft2d(0b1111)
+    y, x = np.meshgrid(np.arange(n), np.arange(n), indexing="ij")
+    want = (1 - 2 * ((x + y) % 2)) * np.exp(2j * np.pi * (300 * x + 7 * y) / n)
+    assert np.abs(cplx(ctx.read(oh.TEX_PLANE0)) - want).max() < 1e-5
+    A, B, L = (cplx(ctx.read(oh.TEX_PLANE0 + p)) for p in (1, 2, 3))
+    assert O.rel_err(L, 2 * A - B) < 2e-6
+    ctx.close()
+
+
+def test_fill_operator():
+    n = 64
+    ctx, _ = make_ctx(n, O.SCENE_CASCADES[:2])
+    rng = np.random.default_rng(2)
+    planes = [(0.1 * rng.standard_normal((2, n, n, 2))).astype(np.float32) for _ in range(4)]
+    turb = np.abs(rng.standard_normal((2, n, n, 4))).astype(np.float32)
+    for p in range(4):
+        for c in range(2):
+            ctx.write(oh.TEX_PLANE0 + p, planes[p][c], 0, c)
+    for c in range(2):
+        ctx.write(oh.TEX_TURB, turb[c], 0, c)
+    ctx.fill()
+    disp, deriv, tb = O.fill(planes, turb)
+    np.testing.assert_array_equal(ctx.read_all(oh.TEX_DISP), disp)
+    np.testing.assert_array_equal(ctx.read_all(oh.TEX_DERIV), deriv)
+    np.testing.assert_array_equal(ctx.read_all(oh.TEX_TURB), tb)
+    ctx.close()
+
+
+# ------------------------------------------------------------- full frame
+@pytest.mark.parametrize("flags", [0, oh.F_UNFUSED])
+def test_golden_fixtures(flags):
+    man = json.load(open(os.path.join(GOLDEN, "manifest.json")))
+    for case in man["cases"]:
+        if case["name"].startswith("ifft"):
+            z = np.load(os.path.join(GOLDEN, case["file"]))
+            ctx = oh.OceanContext(32, 2, 1, flags)
+            for c in range(2):
+                ctx.write(oh.TEX_PLANE0, z["input"][c], 0, c)
+            ctx.ifft2d(1)
+            assert O.rel_err(cplx(ctx.read_all(oh.TEX_PLANE0)), cplx(z["output"])) <= TOL
+            ctx.close()
+            continue
+        z = np.load(os.path.join(GOLDEN, case["file"]))
+        n, full = case["n"], case["nplanes"] == 4
+        ctx = oh.OceanContext(n, len(case["cascades"]), 1, flags | (0 if full else oh.F_DISPLACEMENT_ONLY))
+        ctx.set_params(case["params"], case["cascades"])
+        ctx.generate_noise(case["seed"])
+        np.testing.assert_array_equal(ctx.read(oh.TEX_NOISE), z["noise"])
+        ctx.init_spectrum()
+        for f, t in enumerate(case["times"]):
+            ctx.step(t)
+            assert_channels(ctx.read_all(oh.TEX_DISP)[..., :3], z[f"disp_{f}"][..., :3], what=f"{case['name']} disp {f}")
+            if full:
+                assert_channels(ctx.read_all(oh.TEX_DERIV), z[f"deriv_{f}"], what=f"{case['name']} deriv {f}")
+                assert_channels(ctx.read_all(oh.TEX_TURB), z[f"turb_{f}"], what=f"{case['name']} turb {f}")
+        ctx.close()
+
+
+@pytest.mark.parametrize("n,ncasc,flags", [(256, 1, 0), (512, 1, oh.F_DISPLACEMENT_ONLY), (512, 3, 0),
+                                           (1024, 4, 0), (1024, 4, oh.F_UNFUSED), (2048, 1, 0)])
+def test_frames_vs_oracle(n, ncasc, flags):
+    """BASELINE configs: cfg1-shaped 256^2 x1, cfg2 512^2 displacement only, the scene (512^2 x3),
+    cfg3 4 x 1024^2 full outputs; 3 frames so the foam state is exercised."""
+    cas = O.SCENE_CASCADES[:ncasc]
+    ctx, (noise,) = make_ctx(n, cas, flags=flags)
+    nplanes = 2 if flags & oh.F_DISPLACEMENT_ONLY else 4
+    oc = O.OracleOcean(n, O.scene_params(), cas, noise, nplanes=nplanes)
+    for f, t in enumerate([0.0, 1.0 / 60.0, 100.0]):
+        ctx.step(t)
+        disp, deriv, turb = oc.step(t)
+        assert_channels(ctx.read_all(oh.TEX_DISP)[..., :3], disp[..., :3], what=f"disp f{f}")
+        if nplanes == 4:
+            assert_channels(ctx.read_all(oh.TEX_DERIV), deriv, what=f"deriv f{f}")
+            assert_channels(ctx.read_all(oh.TEX_TURB), turb, what=f"turb f{f}")
+    ctx.close()
+
+
+def test_fused_equals_unfused_to_rounding():
+    n, cas = 256, O.SCENE_CASCADES
+    a, _ = make_ctx(n, cas)
+    b, _ = make_ctx(n, cas, flags=oh.F_UNFUSED)
+    for t in (0.3, 0.6):
+        a.step(t)
+        b.step(t)
+    for tex in (oh.TEX_DISP, oh.TEX_DERIV, oh.TEX_TURB):
+        assert_channels(a.read_all(tex), b.read_all(tex), tol=1e-6, what=f"tex {tex}")
+    a.close()
+    b.close()
+
+
+def test_tiles_are_independent_oceans():
+    """cfg4 shape: T tiles, tile k seeded seed+k; each tile equals a single-tile run."""
+    n, cas, T = 128, O.SCENE_CASCADES, 3
+    ctx = oh.OceanContext(n, 4, T)
+    ctx.set_params(O.scene_params(), cas)
+    ctx.generate_noise(500)
+    ctx.init_spectrum()
+    ctx.step(2.0)
+    for t in range(T):
+        single, _ = make_ctx(n, cas, seeds=[500 + t])
+        single.step(2.0)
+        for tex in (oh.TEX_DISP, oh.TEX_DERIV, oh.TEX_TURB):
+            np.testing.assert_array_equal(ctx.read_all(tex, t), single.read_all(tex))
+        single.close()
+    ctx.close()
+
+
+def test_normals_derived_output():
+    n, cas = 128, O.SCENE_CASCADES[:2]
+    ctx, (noise,) = make_ctx(n, cas, flags=oh.F_NORMALS)
+    ctx.step(0.5)
+    _, deriv, _ = O.OracleOcean(n, O.scene_params(), cas, noise).step(0.5)
+    d = deriv.astype(np.float64)
+    sx, sz = d[..., 0] / (1 + d[..., 2]), d[..., 1] / (1 + d[..., 3])
+    nrm = np.stack([-sx, np.ones_like(sx), -sz], -1)
+    nrm /= np.linalg.norm(nrm, axis=-1, keepdims=True)
+    got = ctx.read_all(oh.TEX_NORMAL)
+    assert np.abs(got[..., :3] - nrm).max() < 1e-4
+    assert np.all(got[..., 3] == 0)
+    ctx.close()
+
+
+def test_flat_sea_foam_converges():
+    n = 64
+    cas = [dict(wavelength=100.0, cutoff_low=1e6, cutoff_high=1e7, swell=0.4, fade=0.1)]
+    ctx, _ = make_ctx(n, cas)
+    for f in range(40):
+        ctx.step(f / 60.0)
+    tb = ctx.read(oh.TEX_TURB)
+    assert np.all(ctx.read(oh.TEX_DISP)[..., :3] == 0)
+    assert abs(float(tb.max()) - 1.0 / (1.0 - np.exp(-2.0))) < 1e-6 and tb.min() == tb.max()
+    ctx.close()
+
+
+def test_foam_state_resume_via_write():
+    """Checkpoint/resume: reading TURB after frame k and writing it into a fresh context
+    reproduces frame k+1 (the only cross-frame state, ResultTexturesFiller.compute:28-32)."""
+    n, cas = 128, O.SCENE_CASCADES[:2]
+    a, _ = make_ctx(n, cas)
+    a.step(0.1)
+    saved = [a.read(oh.TEX_TURB, 0, c) for c in range(2)]
+    a.step(0.2)
+    b, _ = make_ctx(n, cas)
+    for c in range(2):
+        b.write(oh.TEX_TURB, saved[c], 0, c)
+    b.step(0.2)
+    np.testing.assert_array_equal(a.read_all(oh.TEX_TURB), b.read_all(oh.TEX_TURB))
+    a.close()
+    b.close()
+
+
+# ----------------------------------------------------------- host mirror
+def test_water_body_facade_and_get_water_height():
+    wb = oh.scene_water_body(n=256, n_cascades=3, seed=42).Awake()
+    wb.Update(1.5)
+    disp = wb.DisplacementsTextures()
+    assert disp.shape == (3, 256, 256, 4)
+    # WaterBody.cs:199-208 mapping: world (x, z) in [-N/2, N/2] -> texel
+    for wx, wz in [(0.0, 0.0), (-128.0, -128.0), (127.0, 50.0), (500.0, -500.0)]:
+        u = min(max((wx + 128) / 256, 0), 1)
+        v = min(max((wz + 128) / 256, 0), 1)
+        x, y = min(max(int(u * 256), 0), 255), min(max(int(v * 256), 0), 255)
+        assert wb.GetWaterHeight((wx, 0.0, wz)) == disp[0, y, x, 1]
+    wb.windSpeed = 12.0
+    wb.OnValidate()
+    wb.Update(1.5)
+    assert not np.array_equal(wb.DisplacementsTextures(), disp)
+    wb.OnDisable()
+
+
+def test_state_errors():
+    ctx = oh.OceanContext(64, 1, 1)
+    with pytest.raises(oh.OceanError) as ei:
+        ctx.step(0.0)
+    assert ei.value.code == oh.E_STATE
+    with pytest.raises(oh.OceanError) as ei:
+        ctx.init_spectrum()
+    assert ei.value.code == oh.E_STATE
+    import ctypes
+    buf = np.empty(10, np.float32)
+    assert ctx.lib.ocean_read(ctx._h, oh.TEX_DISP, 0, 0, buf.ctypes.data, 40) == oh.E_INVALID_ARG
+    assert ctx.lib.ocean_read(ctx._h, oh.TEX_DISP, 1, 0, buf.ctypes.data, 64 * 64 * 16) == oh.E_INVALID_ARG
+    assert ctx.lib.ocean_read(ctx._h, 99, 0, 0, buf.ctypes.data, 64 * 64 * 16) == oh.E_INVALID_ARG
+    ptr, nbytes = ctx.device_ptr(oh.TEX_DISP)
+    assert ptr and nbytes == 64 * 64 * 16
+    assert ctx.stream() != 0
+    d = oh.OceanContext(64, 1, 1, oh.F_DISPLACEMENT_ONLY)
+    with pytest.raises(oh.OceanError):
+        d.read(oh.TEX_DERIV)
+    _ = ctypes
+    ctx.close()
+    d.close()
+
+
+def test_kernel_timing_counts_launches():
+    ctx, _ = make_ctx(256, O.SCENE_CASCADES)
+    ctx.set_kernel_timing(True)
+    for f in range(5):
+        ctx.step(f / 60)
+    ms_a, na = ctx.kernel_stats(0)
+    ms_b, nb = ctx.kernel_stats(1)
+    assert na == 5 and nb == 5 and ms_a > 0 and ms_b > 0
+    ctx.close()

@@ -1,0 +1,219 @@
+"""CPU tests of the oracle (oracle/ocean_oracle.c): the checker the GPU parity
+tests rely on.  The reference ships no tests or golden vectors (SURVEY.md 4,
+8c), so the oracle is pinned by independent known-answer tests here and by the
+float64 numpy restatement (oracle.ref64), then frozen by tests/golden/."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _cplx(a):
+    return a[..., 0].astype(np.float64) + 1j * a[..., 1].astype(np.float64)
+
+
+# ---------------------------------------------------------------- IFFT KATs
+@pytest.mark.parametrize("n", [16, 32, 64, 256])
+def test_ifft_schedule_equals_numpy_ifft2(n):
+    """IFFT.cs:66-94 == N^2 * ifft2 with the (-1)^(x+y) permute."""
+    rng = np.random.default_rng(n)
+    plane = rng.standard_normal((2, n, n, 2)).astype(np.float32)
+    got = _cplx(O.ifft2d(plane))
+    want = O.ref64.ifft2d(_cplx(plane))
+    assert O.rel_err(got, want) < 2e-6
+
+
+def test_ifft_delta_is_plane_wave():
+    """A single spectral line at (kx, ky) becomes (-1)^(x+y) e^{2 pi i (kx x + ky y)/N}."""
+    n, kx, ky = 32, 3, 5
+    plane = np.zeros((1, n, n, 2), np.float32)
+    plane[0, ky, kx, 0] = 1.0
+    got = _cplx(O.ifft2d(plane))[0]
+    y, x = np.meshgrid(np.arange(n), np.arange(n), indexing="ij")
+    want = (1 - 2 * ((x + y) % 2)) * np.exp(2j * np.pi * (kx * x + ky * y) / n)
+    assert np.abs(got - want).max() < 1e-5
+
+
+def test_ifft_linearity():
+    rng = np.random.default_rng(3)
+    a = rng.standard_normal((1, 64, 64, 2)).astype(np.float32)
+    b = rng.standard_normal((1, 64, 64, 2)).astype(np.float32)
+    lhs = _cplx(O.ifft2d((2 * a + b).astype(np.float32)))
+    rhs = 2 * _cplx(O.ifft2d(a)) + _cplx(O.ifft2d(b))
+    assert O.rel_err(lhs, rhs) < 2e-6
+
+
+def test_twiddle_table_matches_ifft_compute():
+    """PrecomputeTwiddleFactorsAndInputIndices (IFFT.compute:37-45) at N=16, stage 0/last."""
+    n = 16
+    tab = O.twiddle_table(n)
+    assert tab.shape == (4, n, 4)
+    # stage 0: b = N/2, i = y % b, i+b; twiddle exp(-2 pi i * 0) = 1 for y < N/2
+    np.testing.assert_array_equal(tab[0, :8, 2], np.arange(8))
+    np.testing.assert_array_equal(tab[0, :8, 3], np.arange(8) + 8)
+    np.testing.assert_allclose(tab[0, :8, 0], 1.0)
+    np.testing.assert_allclose(tab[0, 8:, 0], -1.0)
+    # last stage: b = 1, i = 2y, twiddle exp(-2 pi i y / N)
+    np.testing.assert_array_equal(tab[3, :8, 2], 2 * np.arange(8))
+    np.testing.assert_allclose(tab[3, :8, 0] + 1j * tab[3, :8, 1], np.exp(-2j * np.pi * np.arange(8) / n), atol=1e-6)
+
+
+# ------------------------------------------------------------ spectrum KATs
+def test_noise_is_standard_normal_and_deterministic():
+    a = O.generate_noise(128, 20251121)
+    b = O.generate_noise(128, 20251121)
+    c = O.generate_noise(128, 20251122)
+    np.testing.assert_array_equal(a, b)
+    assert not np.array_equal(a, c)
+    assert abs(a.mean()) < 0.02 and abs(a.std() - 1.0) < 0.02
+
+
+def test_noise_order_x_outer_y_inner():
+    """WaterBody.cs:90-95: texel (x=i, y=j) filled i-outer, j-inner: texel (0,1) is the 2nd draw pair."""
+    n = 16
+    a = O.generate_noise(n, 5)
+    big = O.generate_noise(n, 5)
+    # first column (x = 0) consumed first; texel (x=0, y=1) equals itself in a larger grid's prefix
+    assert a[1, 0, 0] == big[1, 0, 0]
+    # consumption order check: generating N=16 then reading texels x-outer must be a single stream
+    stream = np.stack([a[j, i] for i in range(n) for j in range(n)])
+    b32 = O.generate_noise(32, 5)
+    stream32 = np.stack([b32[j, i] for i in range(32) for j in range(32)])
+    np.testing.assert_array_equal(stream[:16], stream32[:16])  # same first 16 draw pairs
+
+
+@pytest.mark.parametrize("shallow", [False, True])
+def test_init_spectrum_matches_fp64(shallow):
+    n = 64
+    noise = O.generate_noise(n, 20251121)
+    h0, waves = O.init_spectrum(n, O.scene_params(shallow), O.SCENE_CASCADES, noise)
+    H, W = O.ref64.init_spectrum(n, O.scene_params(shallow), O.SCENE_CASCADES, noise.astype(np.float64))
+    for c in range(4):
+        assert O.rel_err(h0[c], H[c]) < 5e-6
+    assert O.rel_err(waves, W) < 1e-6
+
+
+def test_out_of_band_texels():
+    """Out of band: h0 = 0, waves = (kx, 1, kz, 0) (InitialSpectrum.compute:124-127); k = 0 is out of band."""
+    n = 32
+    noise = O.generate_noise(n, 1)
+    cas = [dict(wavelength=100.0, cutoff_low=0.5, cutoff_high=0.8, swell=0.3, fade=0.1)]
+    h0, waves = O.init_spectrum(n, O.scene_params(), cas, noise)
+    k = np.hypot(waves[0, ..., 0], waves[0, ..., 2])
+    out = (k < 0.5) | (k > 0.8)
+    assert out.any() and (~out).any()
+    assert np.all(h0[0][out] == 0)
+    assert np.all(waves[0][out][:, 1] == 1) and np.all(waves[0][out][:, 3] == 0)
+    assert waves[0, n // 2, n // 2, 1] == 1.0  # k = 0 texel
+
+
+def test_conjugate_index_and_nyquist_self_mirror():
+    """h0.zw = conj(h0.xy at ((N-x)%N, (N-y)%N)); row/column 0 (n = -N/2) mirror onto themselves."""
+    n = 16
+    noise = O.generate_noise(n, 9)
+    cas = [dict(wavelength=20.0, cutoff_low=1e-4, cutoff_high=1e4, swell=0.4, fade=0.0)]
+    h0, _ = O.init_spectrum(n, O.scene_params(), cas, noise)
+    for y in range(n):
+        for x in range(n):
+            mx, my = (n - x) % n, (n - y) % n
+            assert h0[0, y, x, 2] == h0[0, my, mx, 0]
+            assert h0[0, y, x, 3] == -h0[0, my, mx, 1]
+    assert h0[0, 0, 0, 2] == h0[0, 0, 0, 0]  # (0,0) mirrors itself
+
+
+def test_hermitian_spectrum_gives_real_height():
+    """h(k,t) = h0(k) e^{iwt} + conj(h0(-k)) e^{-iwt} is Hermitian once the Nyquist row/column
+    (n = -N/2, which mirrors onto itself) is excluded, so the height field is real."""
+    n = 32
+    noise = O.generate_noise(n, 4)
+    cas = [dict(wavelength=50.0, cutoff_low=1e-3, cutoff_high=2.0, swell=0.4, fade=0.0)]
+    h0, waves = O.init_spectrum(n, O.scene_params(), cas, noise)
+    h0[:, 0, :, :] = 0
+    h0[:, :, 0, :] = 0
+    h0, waves = h0.astype(np.float64), waves.astype(np.float64)
+    e = np.exp(1j * waves[..., 3] * 0.7)
+    h = (h0[..., 0] + 1j * h0[..., 1]) * e + (h0[..., 2] + 1j * h0[..., 3]) * np.conj(e)
+    height = O.ref64.ifft2d(h)
+    assert np.abs(height.imag).max() < 1e-9 * max(np.abs(height.real).max(), 1e-30) + 1e-15
+
+
+@pytest.mark.parametrize("t", [0.0, 1.25])
+def test_frame_matches_fp64(t):
+    n = 64
+    noise = O.generate_noise(n, 20251121)
+    oc = O.OracleOcean(n, O.scene_params(), O.SCENE_CASCADES, noise)
+    disp, deriv, turb = oc.step(t)
+    H, W = O.ref64.init_spectrum(n, O.scene_params(), O.SCENE_CASCADES, noise.astype(np.float64))
+    D, DV, F = O.ref64.frame(H, W, t)
+    for c in range(4):
+        assert O.rel_err(disp[c, ..., :3], D[c]) < 5e-6
+        assert O.rel_err(deriv[c], DV[c]) < 5e-6
+        assert O.rel_err(turb[c, ..., 0], F[c]) < 5e-6
+
+
+def test_frame_large_t_within_fp32_phase_limit():
+    """t = 100 s: fp32 phase w*t differs from fp64 by up to ulp(w t); still within 1e-4."""
+    n = 32
+    noise = O.generate_noise(n, 20251121)
+    oc = O.OracleOcean(n, O.scene_params(), O.SCENE_CASCADES, noise)
+    disp, deriv, _ = oc.step(100.0)
+    H, W = O.ref64.init_spectrum(n, O.scene_params(), O.SCENE_CASCADES, noise.astype(np.float64))
+    D, DV, _ = O.ref64.frame(H, W, 100.0)
+    for c in range(4):
+        assert O.rel_err(disp[c, ..., :3], D[c]) < 1e-4
+
+
+def test_flat_sea_foam_recurrence():
+    """All k out of band -> displacement 0, J = 1, foam 0 -> 1 -> 1 + e^-2 -> ... -> 1/(1 - e^-2)."""
+    n = 16
+    noise = O.generate_noise(n, 2)
+    cas = [dict(wavelength=100.0, cutoff_low=1e6, cutoff_high=1e7, swell=0.4, fade=0.1)]
+    oc = O.OracleOcean(n, O.scene_params(), cas, noise)
+    foam = 0.0
+    for f in range(40):
+        disp, deriv, turb = oc.step(f / 60.0)
+        assert np.all(disp[..., :3] == 0) and np.all(deriv == 0)
+        expect = np.float32(foam) * O.FOAM_DECAY
+        expect = expect + np.float32(1.0) if expect < 1.0 else expect
+        foam = float(expect)
+        assert np.all(turb == np.float32(foam))
+    assert abs(foam - 1.0 / (1.0 - np.exp(-2.0))) < 1e-6
+
+
+def test_displacement_only_matches_full():
+    n = 32
+    noise = O.generate_noise(n, 11)
+    full = O.OracleOcean(n, O.scene_params(), O.SCENE_CASCADES[:2], noise, nplanes=4)
+    disp_only = O.OracleOcean(n, O.scene_params(), O.SCENE_CASCADES[:2], noise, nplanes=2)
+    a, _, _ = full.step(0.3)
+    b, db, tb = disp_only.step(0.3)
+    assert db is None and tb is None
+    np.testing.assert_array_equal(a, b)
+
+
+# ------------------------------------------------------------------ golden
+def test_golden_fixtures_reproduce():
+    """The committed fixtures are exactly what the oracle computes on this host."""
+    man = json.load(open(os.path.join(GOLDEN, "manifest.json")))
+    for case in man["cases"]:
+        z = np.load(os.path.join(GOLDEN, case["file"]))
+        if case["name"].startswith("ifft"):
+            np.testing.assert_array_equal(O.ifft2d(z["input"]), z["output"])
+            continue
+        n = case["n"]
+        noise = O.generate_noise(n, case["seed"])
+        np.testing.assert_array_equal(noise, z["noise"])
+        oc = O.OracleOcean(n, case["params"], case["cascades"], noise, nplanes=case["nplanes"])
+        np.testing.assert_array_equal(oc.h0, z["h0"])
+        np.testing.assert_array_equal(oc.waves, z["waves"])
+        for f, t in enumerate(case["times"]):
+            disp, deriv, turb = oc.step(t)
+            np.testing.assert_array_equal(disp, z[f"disp_{f}"])
+            if case["nplanes"] == 4:
+                np.testing.assert_array_equal(deriv, z[f"deriv_{f}"])
+                np.testing.assert_array_equal(turb, z[f"turb_{f}"])
