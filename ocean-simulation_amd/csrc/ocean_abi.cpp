@@ -5,11 +5,13 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
 #include <vector>
 
+#include "fft_core.h"
 #include "ocean_internal.h"
 
 namespace {
@@ -48,6 +50,7 @@ struct ocean_ctx {
     int device = 0;
     int n = 0, logn = 0, C = 0, T = 0, P = 4;
     uint32_t flags = 0;
+    int variant = 2;  // kernel generation: 1 = fft.hip, 2 = fft2.hip (OCEAN_KERNEL_VARIANT)
     hipStream_t stream = nullptr;
     // device buffers
     float2* noise = nullptr;
@@ -88,6 +91,7 @@ struct ocean_ctx {
         v.h0 = h0;
         v.waves = waves;
         for (int p = 0; p < 4; ++p) v.plane[p] = plane[p];
+        v.plane_stride = texels() * units();
         v.disp = disp;
         v.deriv = deriv;
         v.turb = turb;
@@ -174,8 +178,7 @@ int slice_ptr(ocean_ctx* ctx, int tex, int tile, int cascade, size_t bytes, char
 }
 
 void free_all(ocean_ctx* c) {
-    void* ptrs[] = {c->noise, c->h0, c->waves, c->plane[0], c->plane[1], c->plane[2], c->plane[3],
-                    c->disp,  c->deriv, c->turb, c->normal, c->tw, c->casc};
+    void* ptrs[] = {c->noise, c->h0, c->waves, c->plane[0], c->disp, c->deriv, c->turb, c->normal, c->tw, c->casc};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& t : c->pending) {
@@ -225,6 +228,7 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
     c->flags = flags;
     c->P = (flags & OCEAN_F_DISPLACEMENT_ONLY) ? 2 : 4;
     c->noise_set.assign(n_tiles, false);
+    if (const char* kv = std::getenv("OCEAN_KERNEL_VARIANT")) c->variant = std::atoi(kv) == 1 ? 1 : 2;
 
     auto alloc = [&](void** p, size_t bytes) -> bool {
         if (hipMalloc(p, bytes) != hipSuccess) return false;
@@ -235,14 +239,17 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
     ok = ok && alloc((void**)&c->noise, tex * c->T * 8);
     ok = ok && alloc((void**)&c->h0, tex * U * 16);
     ok = ok && alloc((void**)&c->waves, tex * U * 16);
-    for (int p = 0; p < c->P; ++p) ok = ok && alloc((void**)&c->plane[p], tex * U * 8);
+    ok = ok && alloc((void**)&c->plane[0], tex * U * 8 * c->P);  // planes contiguous (one descriptor in pass A)
+    if (ok)
+        for (int p = 1; p < c->P; ++p) c->plane[p] = c->plane[0] + (size_t)p * tex * U;
     ok = ok && alloc((void**)&c->disp, tex * U * 16);
     if (c->P == 4) {
         ok = ok && alloc((void**)&c->deriv, tex * U * 16);
         ok = ok && alloc((void**)&c->turb, tex * U * 16);
     }
     if (flags & OCEAN_F_NORMALS) ok = ok && alloc((void**)&c->normal, tex * U * 16);
-    ok = ok && alloc((void**)&c->tw, (size_t)n * 8);
+    const size_t tw_entries = (size_t)n + 128 + ocean::stage_twiddle_entries(n);
+    ok = ok && alloc((void**)&c->tw, tw_entries * 8);
     ok = ok && alloc((void**)&c->casc, 5 * 4 * 5);
     if (!ok) {
         std::string msg = std::string("device allocation failed: ") + hipGetErrorString(hipGetLastError());
@@ -251,12 +258,30 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
         return fail(OCEAN_E_OUT_OF_MEMORY, msg);
     }
     // twiddle table tw[m] = exp(+2 pi i m / N), double precision then rounded
-    std::vector<float2> tw(n);
+    std::vector<float2> tw(tw_entries);
     for (int m = 0; m < n; ++m) {
         const double a = 2.0 * M_PI * (double)m / (double)n;
         tw[m] = make_float2((float)std::cos(a), (float)std::sin(a));
     }
-    e = hipMemcpy(c->tw, tw.data(), (size_t)n * 8, hipMemcpyHostToDevice);
+    for (int k = 0; k < 64; ++k) {
+        const double lo = 2.0 * M_PI * (double)k / (double)n, hi = 2.0 * M_PI * 64.0 * (double)k / (double)n;
+        tw[n + k] = make_float2((float)std::cos(lo), (float)std::sin(lo));
+        tw[n + 64 + k] = make_float2((float)std::cos(hi), (float)std::sin(hi));
+    }
+    // per-stage tables: stage s >= 1 (Ns, R), entry r*Ns + k = exp(+2 pi i r k / (Ns R))
+    {
+        using namespace ocean::fftcore;
+        size_t o = (size_t)n + 128;
+        for (int s = 1; s < n_stages(n); ++s) {
+            const int ns = ns_of(n, s), r = radix_of(n, s);
+            for (int q = 0; q < r; ++q)
+                for (int k = 0; k < ns; ++k) {
+                    const double a = 2.0 * M_PI * (double)q * (double)k / ((double)ns * (double)r);
+                    tw[o++] = make_float2((float)std::cos(a), (float)std::sin(a));
+                }
+        }
+    }
+    e = hipMemcpy(c->tw, tw.data(), tw_entries * 8, hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         free_all(c);
         delete c;
@@ -348,8 +373,8 @@ int ocean_ifft2d(ocean_ctx* ctx, int plane_mask) {
     for (int p = 0; p < 4; ++p) {
         if (!(plane_mask & (1 << p))) continue;
         if (p >= ctx->P) return fail(OCEAN_E_INVALID_ARG, "plane not allocated (DISPLACEMENT_ONLY context)");
-        if (int r = timed(ctx, 0, [&] { return ocean::launch_ifft_rows(v, p, ctx->stream); }, "ifft_rows")) return r;
-        if (int r = timed(ctx, 1, [&] { return ocean::launch_ifft_cols(v, p, ctx->stream); }, "ifft_cols")) return r;
+        if (int r = timed(ctx, 0, [&] { return ctx->variant == 2 ? ocean::launch_ifft_rows_v2(v, p, ctx->stream) : ocean::launch_ifft_rows(v, p, ctx->stream); }, "ifft_rows")) return r;
+        if (int r = timed(ctx, 1, [&] { return ctx->variant == 2 ? ocean::launch_ifft_cols_v2(v, p, ctx->stream) : ocean::launch_ifft_cols(v, p, ctx->stream); }, "ifft_cols")) return r;
     }
     return OCEAN_OK;
 }
@@ -369,8 +394,8 @@ int ocean_step(ocean_ctx* ctx, float time) {
         return ocean_fill(ctx);
     }
     const ocean::DevView v = ctx->view();
-    if (int r = timed(ctx, 0, [&] { return ocean::launch_pass_a(v, time, ctx->stream); }, "pass_a")) return r;
-    return timed(ctx, 1, [&] { return ocean::launch_pass_b(v, ctx->stream); }, "pass_b");
+    if (int r = timed(ctx, 0, [&] { return ctx->variant == 2 ? ocean::launch_pass_a_v2(v, time, ctx->stream) : ocean::launch_pass_a(v, time, ctx->stream); }, "pass_a")) return r;
+    return timed(ctx, 1, [&] { return ctx->variant == 2 ? ocean::launch_pass_b_v2(v, ctx->stream) : ocean::launch_pass_b(v, ctx->stream); }, "pass_b");
 }
 
 int ocean_read(ocean_ctx* ctx, int texture, int tile, int cascade, void* dst, size_t bytes) {

@@ -22,12 +22,14 @@ struct DevView {
     const float2* noise;  // [T][N][N]
     float4* h0;           // [U][N][N]
     float4* waves;        // [U][N][N]
-    float2* plane[4];     // [U][N][N] each
+    float2* plane[4];     // [U][N][N] each; one allocation, plane[p] = plane[0] + p * plane_stride
+    size_t plane_stride;  // elements between consecutive planes (U * N * N)
     float4* disp;         // [U][N][N]
     float4* deriv;        // [U][N][N] (full only)
     float4* turb;         // [U][N][N] (full only)
     float4* normal;       // [U][N][N] (normals only)
-    const float2* tw;     // [N] exp(+2 pi i m / N), m < N
+    const float2* tw;     // [N + 128]: exp(+2 pi i m / N), m < N; then T1[64] = exp(2 pi i lo / N),
+                          // T2[64] = exp(2 pi i 64 hi / N) (two-level table for N > 1024)
     const float* casc;    // [C][5] wavelength, cutoff_low, cutoff_high, swell, fade (device)
 };
 
@@ -50,5 +52,13 @@ hipError_t launch_ifft_cols(const DevView& v, int p, hipStream_t s);
 // permute + fill/foam (+ normals).
 hipError_t launch_pass_a(const DevView& v, float t, hipStream_t s);
 hipError_t launch_pass_b(const DevView& v, hipStream_t s);
+
+// fft2.hip: persistent, software-pipelined versions of the same four launches.
+// Entries of the per-stage twiddle tables stored at tw + N + 128 (see fft2.hip StageTw).
+size_t stage_twiddle_entries(int n);
+hipError_t launch_ifft_rows_v2(const DevView& v, int p, hipStream_t s);
+hipError_t launch_ifft_cols_v2(const DevView& v, int p, hipStream_t s);
+hipError_t launch_pass_a_v2(const DevView& v, float t, hipStream_t s);
+hipError_t launch_pass_b_v2(const DevView& v, hipStream_t s);
 
 }  // namespace ocean

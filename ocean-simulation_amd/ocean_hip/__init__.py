@@ -33,7 +33,7 @@ except Exception:  # torch absent: the library then binds to /opt/rocm's runtime
     _torch = None
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liboceanhip.so")
+LIB_PATH = os.environ.get("OCEAN_HIP_LIB") or os.path.join(_HERE, "liboceanhip.so")
 
 OK = 0
 E_INVALID_ARG = -1

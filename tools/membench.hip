@@ -1,0 +1,126 @@
+// Memory-pattern microbenchmark for the ocean path's access shapes on MI355X.
+// Build: hipcc --offload-arch=gfx950 -O3 tools/membench.hip -o tools/membench
+// Each test moves a fixed byte count; prints GB/s (bytes read + written / time).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <vector>
+
+#define CK(x)                                                                         \
+    do {                                                                              \
+        hipError_t e = (x);                                                           \
+        if (e != hipSuccess) {                                                        \
+            printf("HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); \
+            return 1;                                                                 \
+        }                                                                             \
+    } while (0)
+
+constexpr int N = 1024;
+
+// 1. streaming float4 copy (grid-stride)
+__global__ void k_copy(const float4* __restrict__ a, float4* __restrict__ b, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) b[i] = a[i];
+}
+
+// 2. column-tile read of float2 planes: tile = W columns x N rows, lane (b = tid % W, j = tid / W)
+//    reads rows j + 64 r (16 values), writes the same texels (in-place style copy to b)
+template <int W>
+__global__ void k_coltile(const float2* __restrict__ a, float2* __restrict__ b, int tiles_per_unit) {
+    constexpr int T = W * N / 16;
+    const int tile = blockIdx.x;
+    const int u = tile / tiles_per_unit, x0 = (tile % tiles_per_unit) * W;
+    const int lb = threadIdx.x % W, lj = threadIdx.x / W;
+    const float2* src = a + (size_t)u * N * N + x0 + lb;
+    float2* dst = b + (size_t)u * N * N + x0 + lb;
+    constexpr int RS = T / W;  // rows between a lane's values
+    float2 v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = src[(size_t)(lj + r * RS) * N];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dst[(size_t)(lj + r * RS) * N] = v[r];
+}
+
+// 3. column-tile float4 stores (the pass-B epilogue shape): 16 B per lane, W texels per row
+template <int W>
+__global__ void k_coltile_store4(float4* __restrict__ b, int tiles_per_unit) {
+    constexpr int T = W * N / 16;
+    const int tile = blockIdx.x;
+    const int u = tile / tiles_per_unit, x0 = (tile % tiles_per_unit) * W;
+    const int lb = threadIdx.x % W, lj = threadIdx.x / W;
+    float4* dst = b + (size_t)u * N * N + x0 + lb;
+    constexpr int RS = T / W;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dst[(size_t)(lj + r * RS) * N] = make_float4(r, lj, lb, 1.f);
+}
+
+// 4. row read of float2 (the row pass shape): 4 rows per WG, lane reads j + 64 r
+__global__ void k_rowtile(const float2* __restrict__ a, float2* __restrict__ b) {
+    const size_t row0 = (size_t)blockIdx.x * 4;
+    const int rb = threadIdx.x / 64, j = threadIdx.x % 64;
+    const float2* src = a + (row0 + rb) * N + j;
+    float2* dst = b + (row0 + rb) * N + j;
+    float2 v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = src[r * 64];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dst[r * 64] = v[r];
+}
+
+template <class F>
+float timeit(F f, int reps) {
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    f();
+    (void)hipDeviceSynchronize();
+    (void)hipEventRecord(a);
+    for (int i = 0; i < reps; ++i) f();
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, a, b);
+    return ms / reps;
+}
+
+int main() {
+    const int units = 16;  // 16 x 1024^2 complex = 128 MiB per plane array (beyond L2, inside MALL)
+    const size_t elems = (size_t)units * N * N;
+    float2 *a, *b;
+    float4* c;
+    CK(hipMalloc(&a, elems * 8));
+    CK(hipMalloc(&b, elems * 8));
+    CK(hipMalloc(&c, elems * 16));
+    CK(hipMemset(a, 0, elems * 8));
+    CK(hipMemset(b, 0, elems * 8));
+    CK(hipMemset(c, 0, elems * 16));
+    const int reps = 20;
+    {
+        float ms = timeit([&] { hipLaunchKernelGGL(k_copy, dim3(8192), dim3(256), 0, 0, (const float4*)a, (float4*)b, elems / 2); }, reps);
+        printf("copy float4            %8.1f GB/s  (%.1f us)\n", 2.0 * elems * 8 / ms / 1e6, ms * 1e3);
+    }
+    {
+        float ms = timeit([&] { hipLaunchKernelGGL(k_rowtile, dim3(units * N / 4), dim3(256), 0, 0, a, b); }, reps);
+        printf("row tile float2        %8.1f GB/s  (%.1f us)\n", 2.0 * elems * 8 / ms / 1e6, ms * 1e3);
+    }
+    {
+        float ms = timeit([&] { hipLaunchKernelGGL(k_coltile<8>, dim3(units * N / 8), dim3(512), 0, 0, a, b, N / 8); }, reps);
+        printf("col tile W=8 float2    %8.1f GB/s  (%.1f us)\n", 2.0 * elems * 8 / ms / 1e6, ms * 1e3);
+    }
+    {
+        float ms = timeit([&] { hipLaunchKernelGGL(k_coltile<16>, dim3(units * N / 16), dim3(1024), 0, 0, a, b, N / 16); }, reps);
+        printf("col tile W=16 float2   %8.1f GB/s  (%.1f us)\n", 2.0 * elems * 8 / ms / 1e6, ms * 1e3);
+    }
+    {
+        float ms = timeit([&] { hipLaunchKernelGGL(k_coltile<4>, dim3(units * N / 4), dim3(256), 0, 0, a, b, N / 4); }, reps);
+        printf("col tile W=4 float2    %8.1f GB/s  (%.1f us)\n", 2.0 * elems * 8 / ms / 1e6, ms * 1e3);
+    }
+    {
+        float ms = timeit([&] { hipLaunchKernelGGL(k_coltile_store4<8>, dim3(units * N / 8), dim3(512), 0, 0, c, N / 8); }, reps);
+        printf("col tile W=8 store f4  %8.1f GB/s  (%.1f us)\n", 1.0 * elems * 16 / ms / 1e6, ms * 1e3);
+    }
+    {
+        float ms = timeit([&] { hipLaunchKernelGGL(k_coltile_store4<16>, dim3(units * N / 16), dim3(1024), 0, 0, c, N / 16); }, reps);
+        printf("col tile W=16 store f4 %8.1f GB/s  (%.1f us)\n", 1.0 * elems * 16 / ms / 1e6, ms * 1e3);
+    }
+    return 0;
+}
