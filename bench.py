@@ -53,13 +53,40 @@ CONFIGS = {
 
 
 def algorithmic_bytes(n, units, disp_only):
-    """Per-launch algorithmic HBM bytes.
-    pass A: read h0 + waves (32 B), write P planes (8 B each);
-    pass B: read P planes (8 B each) [+ foam 16 B], write disp 16 B [+ deriv 16 B + turb 16 B]."""
+    """Per-launch algorithmic HBM bytes of the fused schedule, N <= 1024 (v3):
+    pass A: read h0 (16 B; wave data is recomputed), write P planes (8 B each);
+    pass B: read P planes (8 B each) [+ foam state 4 B], write DISP 16 B [+ DERIV 16 B + TURB 16 B
+    + foam state 4 B].  N > 1024 (v2 kernels) additionally read the wave data (16 B) in pass A and
+    read TURB (16 B) instead of the compact foam state in pass B."""
     tex = n * n * units
+    wave = 16 if n > 1024 else 0
+    foam = (16, 0) if n > 1024 else (4, 4)
     if disp_only:
-        return {"pass_a": tex * (32 + 16), "pass_b": tex * (16 + 16), "frame": tex * 80}
-    return {"pass_a": tex * (32 + 32), "pass_b": tex * (32 + 16 + 48), "frame": tex * 160}
+        a, b = 16 + wave + 16, 16 + 16
+    else:
+        a, b = 16 + wave + 32, 32 + foam[0] + 48 + foam[1]
+    return {"pass_a": tex * a, "pass_b": tex * b, "frame": tex * (a + b)}
+
+
+def pmc_traffic(kernel_substr, profiles_dir=os.path.join(ROOT, "profiles")):
+    """HBM bytes per launch of a kernel from the newest committed rocprofv3 PMC summary
+    (tools/profile.sh -> profiles/<round>/pmc_summary.json): 2 x FETCH_SIZE (gfx950 reports half
+    of wide streaming reads) + WRITE_SIZE.  None if no summary covers the kernel."""
+    best = None
+    if not os.path.isdir(profiles_dir):
+        return None
+    for d in sorted(os.listdir(profiles_dir)):
+        f = os.path.join(profiles_dir, d, "pmc_summary.json")
+        if not os.path.exists(f):
+            continue
+        try:
+            summ = json.load(open(f))
+        except Exception:
+            continue
+        for k, rec in summ.get("kernels", {}).items():
+            if kernel_substr in k and summ.get("config") == "cfg3":
+                best = (rec["hbm_bytes_per_launch"], d)
+    return best
 
 
 def cpu_baseline(cfg, frames=3):
@@ -183,8 +210,8 @@ def main():
     if args.unfused:
         dom = "ifft_cols" if dom == "pass_b" else "ifft_rows"
     dom_bytes = B["pass_b" if dom in ("pass_b", "ifft_cols") else "pass_a"]
-    if args.unfused:  # unfused row/col kernels move 16 B per texel per plane
-        dom_bytes = n * n * units * 16
+    if args.unfused:  # unfused row/col launches move 16 B per texel per plane, all planes in one launch
+        dom_bytes = n * n * units * 16 * (2 if cfg["disp_only"] else 4)
     achieved = dom_bytes / (dom_us * 1e-6) / 1e9 if dom_us > 0 else 0.0
 
     ifft_stage = None
@@ -207,11 +234,14 @@ def main():
         kern_us = 1e3 * (r_ms + c_ms) / reps
         ifft_stage = {"bytes": fft_bytes, "us_per_stage_wall": round(stage_us, 2),
                       "us_per_stage_kernels": round(kern_us, 2),
-                      "row_kernel_us": round(1e3 * r_ms / max(r_n, 1), 2),
-                      "col_kernel_us": round(1e3 * c_ms / max(c_n, 1), 2),
+                      "row_launch_us_4_planes": round(1e3 * r_ms / max(r_n, 1), 2),
+                      "col_launch_us_4_planes": round(1e3 * c_ms / max(c_n, 1), 2),
                       "achieved_GBs": round(fft_bytes / (kern_us * 1e-6) / 1e9, 1),
                       "frac": round(fft_bytes / (kern_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
 
+    traffic = pmc_traffic(("k_pass_b" if dom == "pass_b" else "k_pass_a") if not args.unfused
+                          else ("k_cols" if dom == "ifft_cols" else "k_rows")) \
+        if (args.config == "cfg3" and not args.unfused) else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg)
@@ -238,7 +268,9 @@ def main():
                        "schedule": "unfused" if args.unfused else "fused (pass A + pass B)",
                        "parallelism": f"independent oceans sharded over {world} GPU(s), no collective"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic[0] if traffic else None,
+                         "traffic_source": f"profiles/{traffic[1]}/pmc_summary.json" if traffic else None,
                          "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_us": round(dom_us, 3)},
             "kernels_us": {"pass_a" if not args.unfused else "rows": round(a_us, 3),
                            "pass_b" if not args.unfused else "cols": round(b_us, 3)},

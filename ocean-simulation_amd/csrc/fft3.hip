@@ -1,0 +1,316 @@
+// v3 fused frame for N <= 1024 (BASELINE cfg2 / cfg3 / cfg4 sizes).
+//
+// Pass A (k_pass_a3): evolve + row IFFT.  A workgroup owns RB = 1024/N
+//   consecutive rows and all P planes of them (256 lanes for P = 4).  The
+//   Stockham plan starts with radix R0 = 16/P so that in stage 0 one lane holds
+//   every plane of R0 texels: the lane evolves those texels
+//   (TimeDependentSpectrum.compute:20-47) and runs the first butterflies on
+//   the results in registers -- no LDS round trip for the evolve.  The wave
+//   data (kx, 1/|k|, kz, omega) is recomputed from (x, y, cascade) with the
+//   init kernel's own arithmetic (spectrum_math.h wave_data, bit-identical)
+//   instead of being read: 16 B/texel less HBM traffic.  Outputs go to the
+//   column-tile-major intermediate [p][u][x/W][y][W], W = col_tile(N)
+//   (64 B runs at N = 1024; 2-row workgroups that write 128 B runs measured
+//   slower: this pass is VALU/latency-bound, not store-bound).
+// Pass B (k_pass_b3): per W-column tile, column IFFT of each plane from one
+//   contiguous 8*W*N-byte block, permute, fill/foam epilogue; the foam state
+//   is a compact float in the same tile-major layout (4 B read + 4 B write
+//   instead of a 16 B RGBA read), TURB is written as its broadcast image.
+//
+// Bytes per texel-cascade (P = 4): pass A 16 (h0) + 32 (planes) = 48;
+// pass B 32 (planes) + 4 + 4 (foam) + 48 (DISP, DERIV, TURB) = 88.
+#include <cstdlib>
+
+#include "fft_engine.h"
+#include "spectrum_math.h"
+
+namespace ocean {
+namespace {
+
+constexpr int pa3_rows(int N, int RS = 2) { return N >= 1024 * RS ? 1 : 1024 * RS / N; }
+
+template <int N, int P, int RS = 1, bool READW = false, bool PF = false, int WPS = 0>
+__global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems, WPS) void k_pass_a3(DevView v, float time,
+                                                                                   int total_rows) {
+    constexpr int RB = pa3_rows(N, RS);
+    constexpr int FIRST = 16 / P;
+    using E = Engine<N, RB * P, false, true, FIRST>;
+    using TW = StageTw<N, FIRST>;
+    constexpr int T = E::THREADS;
+    constexpr int R0 = E::R0;             // = FIRST (texels per lane)
+    constexpr int NJ = N / R0;            // stage-0 butterflies per sequence
+    constexpr int W = col_tile(N);
+    constexpr int TILES = N / W;
+    constexpr int NSL = N / E::RL;        // last-stage Ns
+    static_assert(T / NJ == RB, "stage-0 mapping: lane -> (row, j), butterfly m -> plane m");
+    __shared__ float2 lds[E::LDS_ELEMS];
+    __shared__ float2 twl[TW::kLdsEntries];
+    TW::load(twl, v.tw, threadIdx.x, T);
+    const float2* tws = TW::table(twl, v.tw);
+    const int rr = (int)threadIdx.x / NJ, j = (int)threadIdx.x % NJ;  // stage-0 lane coordinates
+    const int items = (total_rows + RB - 1) / RB;
+
+    float4 h[R0], hn[R0];
+    float4 wv[READW ? R0 : 1], wvn[READW ? R0 : 1];
+    auto load = [&](int item, float4 (&hh)[R0], float4 (&ww)[READW ? R0 : 1]) {
+        const int rows = min(RB, total_rows - item * RB);
+        const Win w = make_win(v.h0 + (size_t)item * RB * N, (unsigned)(rows * N * 16));
+#pragma unroll
+        for (int r = 0; r < R0; ++r) hh[r] = bload4(w, (rr * N + j) * 16, r * NJ * 16);  // past-end rows read 0
+        if constexpr (READW) {
+            const Win w2 = make_win(v.waves + (size_t)item * RB * N, (unsigned)(rows * N * 16));
+#pragma unroll
+            for (int r = 0; r < R0; ++r) ww[r] = bload4(w2, (rr * N + j) * 16, r * NJ * 16);
+        }
+    };
+    int item = blockIdx.x;
+    if (item < items) load(item, h, wv);
+    __syncthreads();  // twiddles
+    for (; item < items; item += gridDim.x) {
+        const int next = item + gridDim.x;
+        if constexpr (PF) {
+            if (next < items) load(next, hn, wvn);
+        }
+        // stage-0 inputs: plane m of texel x = j + r*NJ of row (item*RB + rr)
+        const int row = item * RB + rr;
+        const int u = row / N, y = row % N;
+        const float* cs = v.casc + (u % v.C) * 5;
+        float2 in[kElems];
+#pragma unroll
+        for (int r = 0; r < R0; ++r) {
+            float4 wd;
+            if constexpr (READW) wd = wv[r];
+            else wd = wave_data(j + r * NJ, y, N, cs, v.gravity);
+            const Planes4 o = evolve_texel(h[r], wd, time);
+#pragma unroll
+            for (int m = 0; m < P; ++m) in[m * R0 + r] = o.p[m];
+        }
+        // outputs: sequence b = p*RB + rr', element x -> tplane[p][u'][x/W][y'][x%W]
+        auto emit = [&](int m, int q, float2 val) {
+            int b, jj;
+            E::template bj<E::RL>((int)threadIdx.x + m * T, b, jj);
+            const int p = b / RB, r2 = b % RB;
+            const int row2 = item * RB + r2;
+            if (row2 < total_rows) {
+                const int u2 = row2 / N, y2 = row2 % N;
+                float2* rowp = v.tplane + (size_t)p * v.plane_stride + ((size_t)u2 * TILES * N + y2) * W;
+                if constexpr (NSL % W == 0) {
+                    // x = jj + q*NSL: x/W = jj/W + q*NSL/W, x%W = jj%W (compile-time tile stride)
+                    float2* dst = rowp + (size_t)(jj / W) * N * W + (jj % W);
+                    dst[(size_t)q * (NSL / W) * N * W] = val;
+                } else {
+                    const int x = jj + q * NSL;
+                    rowp[(size_t)(x / W) * N * W + (x % W)] = val;
+                }
+            }
+        };
+        E::run_regs(in, lds, tws, emit);
+        if constexpr (PF) {
+#pragma unroll
+            for (int r = 0; r < R0; ++r) {
+                h[r] = hn[r];
+                if constexpr (READW) wv[r] = wvn[r];
+            }
+        }
+        __syncthreads();
+        if constexpr (!PF) {
+            if (next < items) load(next, h, wv);
+        }
+    }
+}
+
+// Pass B: one item = (unit, W-column tile); planes in the order DyDxz, DxDz,
+// DxxDzz, DyxDyz with the next plane prefetched into registers.
+template <int N, int P>
+__global__ __launch_bounds__(col_tile(N) * N / kElems) void k_pass_b3(DevView v, int items) {
+    using CT = ColTile<N>;
+    using E = typename CT::E;
+    using TW = StageTw<N>;
+    constexpr int W = CT::W;
+    constexpr int T = CT::T;
+    constexpr int RL = CT::RL;
+    constexpr int TILE = W * N;
+    constexpr bool kKeepLds = (E::LDS_ELEMS + TW::kLdsEntries + kElems * T) * 8 <= 160 * 1024;
+    __shared__ float2 lds[E::LDS_ELEMS];
+    __shared__ float2 twl[TW::kLdsEntries];
+    __shared__ float2 keep_lds[kKeepLds ? kElems * T : 1];
+    TW::load(twl, v.tw, threadIdx.x, T);
+    const float2* tws = TW::table(twl, v.tw);
+    constexpr int order[4] = {1, 0, 3, 2};
+    const int lb = CT::lane_b(), lj = CT::lane_j();
+    const int toff = lj * W + lb;                 // lane's element in a tile block
+    const int voff16 = (lj * N + lb) * 16;        // lane's texel in a [y][x] float4 texture window
+
+    float2 keep_reg[kKeepLds ? 1 : kElems];
+    auto kput = [&](int i, float2 x) {
+        if constexpr (kKeepLds) keep_lds[i * T + threadIdx.x] = x;
+        else keep_reg[i] = x;
+    };
+    auto kget = [&](int i) -> float2 {
+        if constexpr (kKeepLds) return keep_lds[i * T + threadIdx.x];
+        else return keep_reg[i];
+    };
+    auto win16 = [&](const float4* base, int item) {
+        const int u = item / CT::tiles, x0 = (item % CT::tiles) * W;
+        return make_win(base + (size_t)u * N * N + x0, (unsigned)((N * N - x0) * 16));
+    };
+    auto load = [&](int item, int p, float2 (&d)[kElems]) {
+        const Win w = make_win(v.tplane + (size_t)p * v.plane_stride + (size_t)item * TILE, TILE * 8);
+#pragma unroll
+        for (int i = 0; i < kElems; ++i) d[i] = bload2(w, toff * 8, CT::in_dy(i) * W * 8);
+    };
+
+    float2 cur[kElems], nxt[kElems];
+    int item = blockIdx.x;
+    if (item < items) load(item, order[0], cur);
+    __syncthreads();
+    for (; item < items; item += gridDim.x) {
+        const int x0 = (item % CT::tiles) * W;
+        float* foam = v.foam + (size_t)item * TILE + toff;
+#pragma unroll
+        for (int pi = 0; pi < P; ++pi) {
+            const int p = order[pi];
+            if (pi + 1 < P) load(item, order[pi + 1], nxt);
+            else if (item + (int)gridDim.x < items) load(item + gridDim.x, order[0], nxt);
+            float fb[kElems];
+            if (p == 3) {
+                const Win rf = make_win(v.foam + (size_t)item * TILE, TILE * 4);
+#pragma unroll
+                for (int m = 0; m < kElems / RL; ++m)
+#pragma unroll
+                    for (int q = 0; q < RL; ++q) fb[m * RL + q] = bload1(rf, toff * 4, CT::out_dy(m, q) * W * 4);
+            }
+            const Win wd = win16(v.disp, item), wt = win16(v.turb, item), wv = win16(v.deriv, item);
+            auto emit = [&](int m, int q, float2 val) {
+                const int i = m * RL + q;
+                const int dy = CT::out_dy(m, q);
+                const float s = perm_sign(x0 + lb, lj + dy);
+                const float re = val.x * s, im = val.y * s;
+                const int so = dy * N * 16;
+                if (p == 1) {  // DyDxz: keep Dy, Dxz
+                    kput(i, make_float2(re, im));
+                } else if (p == 0) {  // DxDz: DISP = (Dx, Dy, Dz, 1)
+                    gstore4(make_float4(re, kget(i).x, im, 1.0f), wd, voff16, so);
+                } else if (p == 3) {  // DxxDzz: foam (needs Dxz), then keep Dxx, Dzz
+                    const float f = foam_update(fb[i], re, im, kget(i).y);
+                    foam[dy * W] = f;
+                    gstore4(make_float4(f, f, f, f), wt, voff16, so);
+                    kput(i, make_float2(re, im));
+                } else {  // DyxDyz: DERIV = (Dyx, Dyz, Dxx, Dzz), NORMAL
+                    const float2 k = kget(i);
+                    gstore4(make_float4(re, im, k.x, k.y), wv, voff16, so);
+                    if (v.normals) gstore4(normal_from_deriv(re, im, k.x, k.y), win16(v.normal, item), voff16, so);
+                }
+            };
+            E::run_regs(cur, lds, tws, emit);
+#pragma unroll
+            for (int i = 0; i < kElems; ++i) cur[i] = nxt[i];
+            __syncthreads();
+        }
+    }
+}
+
+int num_cus3() {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+    }
+    return cus;
+}
+
+template <class K>
+int grid3(K kernel, int threads, int items) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0) != hipSuccess || per_cu <= 0)
+        per_cu = 1;
+    const int g = num_cus3() * per_cu;
+    return items < g ? items : g;
+}
+
+template <int N, int P, int RS = 1, bool READW = false, bool PF = false, int WPS = 0>
+hipError_t go_a3k(const DevView& v, float t, hipStream_t s) {
+    constexpr int RB = pa3_rows(N, RS);
+    constexpr int T = RB * P * N / kElems;
+    const int total = v.units * N;
+    const int items = (total + RB - 1) / RB;
+    const int g = grid3(k_pass_a3<N, P, RS, READW, PF, WPS>, T, items);
+    hipLaunchKernelGGL((k_pass_a3<N, P, RS, READW, PF, WPS>), dim3(g), dim3(T), 0, s, v, t, total);
+    return hipGetLastError();
+}
+
+int a3_variant() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = std::getenv("OCEAN_A3_VARIANT");
+        v = e ? std::atoi(e) : 0;
+    }
+    return v;
+}
+
+template <int N, int P>
+hipError_t go_a3(const DevView& v, float t, hipStream_t s) {
+    if constexpr (N == 1024 && P == 4) {
+        switch (a3_variant()) {
+            // measured on MI355X, 4 x 1024^2 (profiles/r01_*): RB=1 without prefetch is the default
+            case 1: return go_a3k<N, P, 2, false, true>(v, t, s);   // 2 rows / WG, prefetch: +18 %
+            case 2: return go_a3k<N, P, 2, true, true>(v, t, s);    // + wave data read, not recomputed
+            case 3: return go_a3k<N, P, 1, false, true>(v, t, s);   // prefetch
+            case 4: return go_a3k<N, P, 1, true, false>(v, t, s);   // wave data read
+            default: break;
+        }
+    }
+    return go_a3k<N, P>(v, t, s);
+}
+
+template <int N, int P>
+hipError_t go_b3(const DevView& v, hipStream_t s) {
+    constexpr int W = col_tile(N);
+    constexpr int T = W * N / kElems;
+    const int items = v.units * (N / W);
+    const int g = grid3(k_pass_b3<N, P>, T, items);
+    hipLaunchKernelGGL((k_pass_b3<N, P>), dim3(g), dim3(T), 0, s, v, items);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+bool pass_v3_supported(int n) { return n >= 16 && n <= 1024; }
+
+hipError_t launch_pass_a_v3(const DevView& v, float t, hipStream_t s) {
+#define OCEAN_A3(NN)                                                                 \
+    case NN:                                                                         \
+        return v.planes == 4 ? go_a3<NN, 4>(v, t, s) : go_a3<NN, 2>(v, t, s);
+    switch (v.n) {
+        OCEAN_A3(16)
+        OCEAN_A3(32)
+        OCEAN_A3(64)
+        OCEAN_A3(128)
+        OCEAN_A3(256)
+        OCEAN_A3(512)
+        OCEAN_A3(1024)
+    }
+#undef OCEAN_A3
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_pass_b_v3(const DevView& v, hipStream_t s) {
+#define OCEAN_B3(NN)                                                              \
+    case NN:                                                                      \
+        return v.planes == 4 ? go_b3<NN, 4>(v, s) : go_b3<NN, 2>(v, s);
+    switch (v.n) {
+        OCEAN_B3(16)
+        OCEAN_B3(32)
+        OCEAN_B3(64)
+        OCEAN_B3(128)
+        OCEAN_B3(256)
+        OCEAN_B3(512)
+        OCEAN_B3(1024)
+    }
+#undef OCEAN_B3
+    return hipErrorInvalidValue;
+}
+
+}  // namespace ocean

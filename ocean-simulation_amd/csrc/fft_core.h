@@ -11,11 +11,15 @@ namespace fftcore {
 constexpr int kElems = 16;  // complex values held per lane per stage
 
 constexpr int ilog2(int n) { return n <= 1 ? 0 : 1 + ilog2(n / 2); }
-constexpr int n_stages(int N) { return (ilog2(N) + 3) / 4; }
-constexpr int radix_of(int N, int s) {
-    return s < n_stages(N) - 1 ? 16 : (1 << (ilog2(N) - 4 * (n_stages(N) - 1)));
+// Stockham plan: first stage radix R0 (16, 8 or 4), then radix-16 stages, the
+// remainder (2/4/8/16) last.  R0 = 16 is the plain plan; the fused row pass
+// uses R0 = 16 / planes so one lane holds every plane of its texels in stage 0.
+constexpr int n_stages(int N, int R0 = 16) { return N <= R0 ? 1 : 1 + (ilog2(N) - ilog2(R0) + 3) / 4; }
+constexpr int radix_of(int N, int s, int R0 = 16) {
+    return s == 0 ? (N <= R0 ? N : R0)
+                  : (s < n_stages(N, R0) - 1 ? 16 : (1 << (ilog2(N) - ilog2(R0) - 4 * (n_stages(N, R0) - 2))));
 }
-constexpr int ns_of(int N, int s) { return s == 0 ? 1 : ns_of(N, s - 1) * radix_of(N, s - 1); }
+constexpr int ns_of(int N, int s, int R0 = 16) { return s == 0 ? 1 : ns_of(N, s - 1, R0) * radix_of(N, s - 1, R0); }
 __device__ __forceinline__ int pad(int i) { return i + (i >> 4); }
 constexpr int padded(int n) { return n + (n >> 4); }
 

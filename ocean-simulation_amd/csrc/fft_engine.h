@@ -1,0 +1,235 @@
+// FFT engine shared by fft2.hip and fft3.hip: memory-op helpers, per-stage
+// twiddle tables, the LDS Stockham engine and the column-tile geometry.
+// See fft2.hip for the design notes.
+#pragma once
+
+#include "fft_core.h"
+#include "ocean_internal.h"
+
+namespace ocean {
+namespace {
+using namespace fftcore;
+
+// ---------------------------------------------------------- memory ops
+// Stores go through plain global stores: on gfx950 / ROCm 7.2 the raw
+// buffer_store_dwordx4 path with a scalar soffset produced corrupted texels
+// (store data VGPRs overwritten by the following VALU before the store read
+// them; reproduced with tools/dbg_passb.py, loads unaffected) -- DESIGN.md.
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef unsigned int u32x2 __attribute__((__vector_size__(2 * sizeof(unsigned int))));
+typedef unsigned int u32x4 __attribute__((__vector_size__(4 * sizeof(unsigned int))));
+
+// A texture window: buffer descriptor (loads) + base pointer (stores).
+struct Win {
+    rsrc_t r;
+    char* p;
+};
+__device__ __forceinline__ Win make_win(const void* base, unsigned bytes) {
+    Win w;
+    w.r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
+    w.p = (char*)const_cast<void*>(base);
+    return w;
+}
+__device__ __forceinline__ float2 bload2(const Win& w, int voff, int soff) {
+    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(w.r, voff, soff, 0);
+    return make_float2(__uint_as_float(v[0]), __uint_as_float(v[1]));
+}
+__device__ __forceinline__ float4 bload4(const Win& w, int voff, int soff) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(w.r, voff, soff, 0);
+    return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+}
+__device__ __forceinline__ float bload1(const Win& w, int voff, int soff) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(w.r, voff, soff, 0));
+}
+__device__ __forceinline__ void gstore2(float2 x, const Win& w, int voff, int soff) {
+    *(float2*)(w.p + voff + soff) = x;
+}
+__device__ __forceinline__ void gstore4(float4 x, const Win& w, int voff, int soff) {
+    *(float4*)(w.p + voff + soff) = x;
+}
+
+// ------------------------------------------------------------- twiddles
+// Per-stage tables, stage s >= 1 (Ns, R): entry r*Ns + k = exp(+2 pi i r k / (Ns R)),
+// k < Ns, r < R (r-major: lanes with consecutive k read consecutive entries,
+// bank-conflict free; a butterfly's R-1 twiddles sit at compile-time strides);
+// stages concatenated.  Built on the host in double precision
+// at tw + N + 128 (ocean_abi.cpp).
+template <int N, int R0 = 16>
+struct StageTw {
+    static constexpr int S = n_stages(N, R0);
+    static constexpr int off(int s) {
+        return s <= 1 ? 0 : off(s - 1) + ns_of(N, s - 1, R0) * radix_of(N, s - 1, R0);
+    }
+    static constexpr int kEntries = off(S) > 0 ? off(S) : 1;
+    static constexpr bool kInLds = kEntries * 8 <= 20 * 1024;
+    static constexpr int kLdsEntries = kInLds ? kEntries : 1;
+    // table sets for R0 = 16, 8, 4 follow each other at tw + N + 128
+    static constexpr int base() {
+        return R0 == 16 ? 0
+                        : (R0 == 8 ? StageTw<N, 16>::off(n_stages(N, 16))
+                                   : StageTw<N, 16>::off(n_stages(N, 16)) + StageTw<N, 8>::off(n_stages(N, 8)));
+    }
+    static __device__ __forceinline__ const float2* global_table(const float2* tw) { return tw + N + 128 + base(); }
+    static __device__ __forceinline__ void load(float2* lds, const float2* __restrict__ tw, int tid, int nthreads) {
+        if constexpr (kInLds) {
+            const float2* src = global_table(tw);
+            for (int i = tid; i < kEntries; i += nthreads) lds[i] = src[i];
+        }
+    }
+    // table to read from: the LDS copy when it fits, else global memory (L1/L2 resident)
+    static __device__ __forceinline__ const float2* table(const float2* lds, const float2* tw) {
+        if constexpr (kInLds) return lds;
+        else return global_table(tw);
+    }
+};
+
+// --------------------------------------------------------------- engine
+// A workgroup transforms B sequences of length N with THREADS = B*N/16
+// lanes, 16 complex values per lane per stage.  Lane -> (sequence b,
+// butterfly j) is b-fastest (SEQ_FAST, column tiles) or j-fastest (rows).
+// Stage-0 input slot m*R0 + r is element y = j_m + r*N/R0 of sequence b_m;
+// last-stage output slot (m, q) is element y = j_m + q*N/RL.
+template <int N, int B, bool SEQ_FAST, bool PAD, int FIRST = 16>
+struct Engine {
+    static constexpr int THREADS = B * N / kElems;
+    static constexpr int S = n_stages(N, FIRST);
+    static constexpr int R0 = radix_of(N, 0, FIRST);
+    static constexpr int RL = radix_of(N, S - 1, FIRST);
+    static constexpr int LDS_ELEMS = PAD ? padded(B * N) : B * N;
+
+    template <int R>
+    static __device__ __forceinline__ void bj(int g, int& b, int& j) {
+        if constexpr (SEQ_FAST) {
+            b = g % B;
+            j = g / B;
+        } else {
+            b = g / (N / R);
+            j = g % (N / R);
+        }
+    }
+    static __device__ __forceinline__ int raw(int b, int y) { return SEQ_FAST ? y * B + b : b * N + y; }
+    static __device__ __forceinline__ int lidx(int b, int y) { return PAD ? pad(raw(b, y)) : raw(b, y); }
+    // LDS offset of the k-th element at raw-index stride rs from a butterfly's
+    // base element.  Unpadded: k*rs.  Padded rows (i + i/16): every Stockham
+    // access pattern here has power-of-two strides with the base placed so
+    // that (base % 16) + (k*rs % 16) < 16, hence pad(base + k*rs) =
+    // pad(base) + k*rs + (k*rs)/16 -- a compile-time offset.
+    static constexpr int loff(int k, int rs) { return PAD ? k * rs + (k * rs) / 16 : k * rs; }
+    static constexpr bool linear() { return !PAD || !SEQ_FAST; }
+
+    // Stages ST.. from LDS; the last stage hands (m, q, value) to emit.
+    template <int ST, class Emit>
+    static __device__ __forceinline__ void stages_from(float2* lds, const float2* tws, Emit& emit) {
+        constexpr int R = radix_of(N, ST, FIRST);
+        constexpr int NS = ns_of(N, ST, FIRST);
+        constexpr int BF = kElems / R;
+        constexpr bool LAST = (ST == S - 1);
+        constexpr int RD = (SEQ_FAST ? B : 1) * (N / R);  // raw stride between a butterfly's inputs
+        constexpr int WR = (SEQ_FAST ? B : 1) * NS;       // raw stride between its outputs
+        float2 v[kElems];
+#pragma unroll
+        for (int m = 0; m < BF; ++m) {
+            int b, j;
+            bj<R>((int)threadIdx.x + m * THREADS, b, j);
+            if constexpr (linear()) {
+                const float2* src = lds + lidx(b, j);
+#pragma unroll
+                for (int r = 0; r < R; ++r) v[m * R + r] = src[loff(r, RD)];
+            } else {
+#pragma unroll
+                for (int r = 0; r < R; ++r) v[m * R + r] = lds[lidx(b, j + r * (N / R))];
+            }
+        }
+        if constexpr (!LAST) __syncthreads();
+#pragma unroll
+        for (int m = 0; m < BF; ++m) {
+            int b, j;
+            bj<R>((int)threadIdx.x + m * THREADS, b, j);
+            if constexpr (NS > 1) {
+                const float2* t = tws + StageTw<N, FIRST>::off(ST) + (j & (NS - 1));
+#pragma unroll
+                for (int r = 1; r < R; ++r) v[m * R + r] = cmul(v[m * R + r], t[r * NS]);
+            }
+            Idft<R>::run(&v[m * R]);
+            if constexpr (LAST) {
+#pragma unroll
+                for (int q = 0; q < R; ++q) emit(m, q, v[m * R + q]);
+            } else {
+                const int y0 = (j / NS) * NS * R + (j & (NS - 1));
+                if constexpr (linear()) {
+                    float2* dst = lds + lidx(b, y0);
+#pragma unroll
+                    for (int q = 0; q < R; ++q) dst[loff(q, WR)] = v[m * R + q];
+                } else {
+#pragma unroll
+                    for (int q = 0; q < R; ++q) lds[lidx(b, y0 + q * NS)] = v[m * R + q];
+                }
+            }
+        }
+        if constexpr (!LAST) {
+            __syncthreads();
+            stages_from<ST + 1>(lds, tws, emit);
+        }
+    }
+
+    // Stage-0 outputs of butterfly m to LDS (Ns = 1: y = R0 j + q).
+    static __device__ __forceinline__ void stage0_store(float2* lds, int m, const float2* v) {
+        int b, j;
+        bj<R0>((int)threadIdx.x + m * THREADS, b, j);
+        if constexpr (linear()) {
+            float2* dst = lds + lidx(b, j * R0);
+#pragma unroll
+            for (int q = 0; q < R0; ++q) dst[loff(q, SEQ_FAST ? B : 1)] = v[q];
+        } else {
+#pragma unroll
+            for (int q = 0; q < R0; ++q) lds[lidx(b, j * R0 + q)] = v[q];
+        }
+    }
+
+    // Full transform from registers (stage-0 layout); LDS free on entry.
+    template <class Emit>
+    static __device__ __forceinline__ void run_regs(float2 (&v)[kElems], float2* lds, const float2* tws, Emit& emit) {
+        constexpr int BF = kElems / R0;
+#pragma unroll
+        for (int m = 0; m < BF; ++m) Idft<R0>::run(&v[m * R0]);
+        if constexpr (S == 1) {
+#pragma unroll
+            for (int m = 0; m < BF; ++m)
+#pragma unroll
+                for (int q = 0; q < R0; ++q) emit(m, q, v[m * R0 + q]);
+        } else {
+#pragma unroll
+            for (int m = 0; m < BF; ++m) stage0_store(lds, m, &v[m * R0]);
+            __syncthreads();
+            stages_from<1>(lds, tws, emit);
+        }
+    }
+
+    template <class Emit>
+    static __device__ __forceinline__ void run_lds(float2* lds, const float2* tws, Emit& emit) {
+        stages_from<0>(lds, tws, emit);
+    }
+};
+
+__device__ __forceinline__ float perm_sign(int x, int y) { return ((x + y) & 1) ? -1.0f : 1.0f; }
+
+// ------------------------------------------------------ column-tile I/O
+// Column tile = W columns x N rows of one unit.  Lane (b, j) with b = tid % W,
+// j = tid / W for every stage; element (b, y) of the tile lives at texel
+// (x0 + b, y).  Stage-0 inputs are rows j + in_dy(r); last-stage outputs are
+// rows j + out_dy(m, q): the lane's base texel plus compile-time offsets.
+template <int N, int WW = col_tile(N)>
+struct ColTile {
+    static constexpr int W = WW;
+    static constexpr int tiles = N / W;
+    using E = Engine<N, W, true, false>;
+    static constexpr int T = E::THREADS;
+    static constexpr int R0 = E::R0, RL = E::RL;
+    static __device__ __forceinline__ int lane_b() { return (int)threadIdx.x % W; }
+    static __device__ __forceinline__ int lane_j() { return (int)threadIdx.x / W; }
+    static constexpr int out_dy(int m, int q) { return m * (T / W) + q * (N / RL); }
+    static constexpr int in_dy(int r) { return r * (N / R0); }
+};
+
+}  // namespace
+}  // namespace ocean

@@ -63,6 +63,8 @@ struct ocean_ctx {
     float4* normal = nullptr;
     float2* tw = nullptr;
     float* casc = nullptr;
+    float2* tplane = nullptr;  // fused-path intermediate (tile-major), P planes
+    float* foam = nullptr;     // foam state (tile-major)
     // host state
     ocean::SpectrumParams params{};
     bool params_set = false;
@@ -98,6 +100,10 @@ struct ocean_ctx {
         v.normal = normal;
         v.tw = tw;
         v.casc = casc;
+        v.gravity = params.gravity;
+        v.tile_w = ocean::fftcore::col_tile(n);
+        v.tplane = tplane;
+        v.foam = foam;
         return v;
     }
 
@@ -178,7 +184,8 @@ int slice_ptr(ocean_ctx* ctx, int tex, int tile, int cascade, size_t bytes, char
 }
 
 void free_all(ocean_ctx* c) {
-    void* ptrs[] = {c->noise, c->h0, c->waves, c->plane[0], c->disp, c->deriv, c->turb, c->normal, c->tw, c->casc};
+    void* ptrs[] = {c->noise, c->h0,     c->waves, c->plane[0], c->disp, c->deriv,
+                    c->turb,  c->normal, c->tw,    c->casc,     c->tplane, c->foam};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& t : c->pending) {
@@ -246,7 +253,9 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
     if (c->P == 4) {
         ok = ok && alloc((void**)&c->deriv, tex * U * 16);
         ok = ok && alloc((void**)&c->turb, tex * U * 16);
+        ok = ok && alloc((void**)&c->foam, tex * U * 4);
     }
+    if (ocean::pass_v3_supported(n)) ok = ok && alloc((void**)&c->tplane, tex * U * 8 * c->P);
     if (flags & OCEAN_F_NORMALS) ok = ok && alloc((void**)&c->normal, tex * U * 16);
     const size_t tw_entries = (size_t)n + 128 + ocean::stage_twiddle_entries(n);
     ok = ok && alloc((void**)&c->tw, tw_entries * 8);
@@ -268,18 +277,20 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
         tw[n + k] = make_float2((float)std::cos(lo), (float)std::sin(lo));
         tw[n + 64 + k] = make_float2((float)std::cos(hi), (float)std::sin(hi));
     }
-    // per-stage tables: stage s >= 1 (Ns, R), entry r*Ns + k = exp(+2 pi i r k / (Ns R))
+    // per-stage tables for the plans with first radix 16, 8 and 4 (fft_engine.h StageTw):
+    // stage s >= 1 (Ns, R), entry r*Ns + k = exp(+2 pi i r k / (Ns R))
     {
         using namespace ocean::fftcore;
         size_t o = (size_t)n + 128;
-        for (int s = 1; s < n_stages(n); ++s) {
-            const int ns = ns_of(n, s), r = radix_of(n, s);
-            for (int q = 0; q < r; ++q)
-                for (int k = 0; k < ns; ++k) {
-                    const double a = 2.0 * M_PI * (double)q * (double)k / ((double)ns * (double)r);
-                    tw[o++] = make_float2((float)std::cos(a), (float)std::sin(a));
-                }
-        }
+        for (int r0 : {16, 8, 4})
+            for (int s = 1; s < n_stages(n, r0); ++s) {
+                const int ns = ns_of(n, s, r0), r = radix_of(n, s, r0);
+                for (int q = 0; q < r; ++q)
+                    for (int k = 0; k < ns; ++k) {
+                        const double a = 2.0 * M_PI * (double)q * (double)k / ((double)ns * (double)r);
+                        tw[o++] = make_float2((float)std::cos(a), (float)std::sin(a));
+                    }
+            }
     }
     e = hipMemcpy(c->tw, tw.data(), tw_entries * 8, hipMemcpyHostToDevice);
     if (e != hipSuccess) {
@@ -355,6 +366,7 @@ int ocean_init_spectrum(ocean_ctx* ctx) {
         return r;
     if (int r = timed(ctx, 2, [&] { return ocean::launch_conjugate(v, ctx->stream); }, "conjugate")) return r;
     if (ctx->turb) OCEAN_HIP(hipMemsetAsync(ctx->turb, 0, ctx->texels() * ctx->units() * 16, ctx->stream));
+    if (ctx->foam) OCEAN_HIP(hipMemsetAsync(ctx->foam, 0, ctx->texels() * ctx->units() * 4, ctx->stream));
     ctx->spectrum_ready = true;
     return OCEAN_OK;
 }
@@ -369,12 +381,31 @@ int ocean_evolve(ocean_ctx* ctx, float time) {
 int ocean_ifft2d(ocean_ctx* ctx, int plane_mask) {
     if (int r = enter(ctx)) return r;
     if (plane_mask < 0 || plane_mask > 15) return fail(OCEAN_E_INVALID_ARG, "plane_mask must be in [0, 15]");
+    for (int p = 0; p < 4; ++p)
+        if ((plane_mask & (1 << p)) && p >= ctx->P)
+            return fail(OCEAN_E_INVALID_ARG, "plane not allocated (DISPLACEMENT_ONLY context)");
     const ocean::DevView v = ctx->view();
-    for (int p = 0; p < 4; ++p) {
-        if (!(plane_mask & (1 << p))) continue;
-        if (p >= ctx->P) return fail(OCEAN_E_INVALID_ARG, "plane not allocated (DISPLACEMENT_ONLY context)");
-        if (int r = timed(ctx, 0, [&] { return ctx->variant == 2 ? ocean::launch_ifft_rows_v2(v, p, ctx->stream) : ocean::launch_ifft_rows(v, p, ctx->stream); }, "ifft_rows")) return r;
-        if (int r = timed(ctx, 1, [&] { return ctx->variant == 2 ? ocean::launch_ifft_cols_v2(v, p, ctx->stream) : ocean::launch_ifft_cols(v, p, ctx->stream); }, "ifft_cols")) return r;
+    for (int p = 0; p < 4;) {
+        if (!(plane_mask & (1 << p))) {
+            ++p;
+            continue;
+        }
+        int np = 1;  // run of consecutive planes: one launch per direction (planes are one allocation)
+        while (p + np < 4 && (plane_mask & (1 << (p + np)))) ++np;
+        if (ctx->variant == 2) {
+            if (int r = timed(ctx, 0, [&] { return ocean::launch_ifft_rows_v2(v, p, np, ctx->stream); }, "ifft_rows"))
+                return r;
+            if (int r = timed(ctx, 1, [&] { return ocean::launch_ifft_cols_v2(v, p, np, ctx->stream); }, "ifft_cols"))
+                return r;
+        } else {
+            for (int q = p; q < p + np; ++q) {
+                if (int r = timed(ctx, 0, [&] { return ocean::launch_ifft_rows(v, q, ctx->stream); }, "ifft_rows"))
+                    return r;
+                if (int r = timed(ctx, 1, [&] { return ocean::launch_ifft_cols(v, q, ctx->stream); }, "ifft_cols"))
+                    return r;
+            }
+        }
+        p += np;
     }
     return OCEAN_OK;
 }
@@ -394,8 +425,17 @@ int ocean_step(ocean_ctx* ctx, float time) {
         return ocean_fill(ctx);
     }
     const ocean::DevView v = ctx->view();
-    if (int r = timed(ctx, 0, [&] { return ctx->variant == 2 ? ocean::launch_pass_a_v2(v, time, ctx->stream) : ocean::launch_pass_a(v, time, ctx->stream); }, "pass_a")) return r;
-    return timed(ctx, 1, [&] { return ctx->variant == 2 ? ocean::launch_pass_b_v2(v, ctx->stream) : ocean::launch_pass_b(v, ctx->stream); }, "pass_b");
+    const bool v3 = ctx->variant == 2 && ocean::pass_v3_supported(ctx->n);
+    if (int r = timed(ctx, 0, [&] {
+            return v3 ? ocean::launch_pass_a_v3(v, time, ctx->stream)
+                      : ctx->variant == 2 ? ocean::launch_pass_a_v2(v, time, ctx->stream)
+                                          : ocean::launch_pass_a(v, time, ctx->stream);
+        }, "pass_a"))
+        return r;
+    return timed(ctx, 1, [&] {
+        return v3 ? ocean::launch_pass_b_v3(v, ctx->stream)
+                  : ctx->variant == 2 ? ocean::launch_pass_b_v2(v, ctx->stream) : ocean::launch_pass_b(v, ctx->stream);
+    }, "pass_b");
 }
 
 int ocean_read(ocean_ctx* ctx, int texture, int tile, int cascade, void* dst, size_t bytes) {
@@ -416,6 +456,11 @@ int ocean_write(ocean_ctx* ctx, int texture, int tile, int cascade, const void* 
     OCEAN_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
     OCEAN_HIP(hipStreamSynchronize(ctx->stream));
     if (texture == OCEAN_TEX_NOISE) ctx->noise_set[tile] = true;
+    if (texture == OCEAN_TEX_TURB) {  // foam state follows the uploaded TURB.x (resume)
+        const ocean::DevView v = ctx->view();
+        OCEAN_HIP(ocean::launch_foam_import(v, ctx->stream));
+        OCEAN_HIP(hipStreamSynchronize(ctx->stream));
+    }
     return OCEAN_OK;
 }
 

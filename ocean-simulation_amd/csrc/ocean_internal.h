@@ -31,6 +31,10 @@ struct DevView {
     const float2* tw;     // [N + 128]: exp(+2 pi i m / N), m < N; then T1[64] = exp(2 pi i lo / N),
                           // T2[64] = exp(2 pi i 64 hi / N) (two-level table for N > 1024)
     const float* casc;    // [C][5] wavelength, cutoff_low, cutoff_high, swell, fade (device)
+    float gravity;        // for the per-frame wave-data recompute (fused row pass)
+    int tile_w;           // column-tile width W = col_tile(N) of the tile-major layouts below
+    float2* tplane;       // fused intermediate, P planes x [U][N/W][N][W] (tile-major), stride plane_stride
+    float* foam;          // foam state, [U][N/W][N][W] (tile-major); TURB is its broadcast RGBA image
 };
 
 struct SpectrumParams {
@@ -42,6 +46,7 @@ hipError_t launch_init_spectrum(const DevView& v, const SpectrumParams& p, hipSt
 hipError_t launch_conjugate(const DevView& v, hipStream_t s);
 hipError_t launch_evolve(const DevView& v, float t, hipStream_t s);
 hipError_t launch_fill(const DevView& v, hipStream_t s);
+hipError_t launch_foam_import(const DevView& v, hipStream_t s);
 
 // fft.hip
 // Standalone operator (IFFT.InverseFastFourierTransform): in-place row pass and
@@ -56,9 +61,17 @@ hipError_t launch_pass_b(const DevView& v, hipStream_t s);
 // fft2.hip: persistent, software-pipelined versions of the same four launches.
 // Entries of the per-stage twiddle tables stored at tw + N + 128 (see fft2.hip StageTw).
 size_t stage_twiddle_entries(int n);
-hipError_t launch_ifft_rows_v2(const DevView& v, int p, hipStream_t s);
-hipError_t launch_ifft_cols_v2(const DevView& v, int p, hipStream_t s);
+// v2 operator launches cover `np` consecutive planes p .. p+np-1 (one allocation) in one launch.
+hipError_t launch_ifft_rows_v2(const DevView& v, int p, int np, hipStream_t s);
+hipError_t launch_ifft_cols_v2(const DevView& v, int p, int np, hipStream_t s);
 hipError_t launch_pass_a_v2(const DevView& v, float t, hipStream_t s);
 hipError_t launch_pass_b_v2(const DevView& v, hipStream_t s);
+
+// fft3.hip (N <= 1024): fused frame through the tile-major intermediate; the
+// row pass recomputes wave data and feeds evolve straight into a radix-4/8
+// first stage; the column pass reads contiguous tiles and the compact foam state.
+bool pass_v3_supported(int n);
+hipError_t launch_pass_a_v3(const DevView& v, float t, hipStream_t s);
+hipError_t launch_pass_b_v3(const DevView& v, hipStream_t s);
 
 }  // namespace ocean

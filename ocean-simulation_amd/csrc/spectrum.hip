@@ -17,7 +17,7 @@ struct Sp {
     float U, g, F, D, wdx, wdy;
 };
 
-__device__ __forceinline__ float angular_frequency(const Sp& p, float k) { return sqrtf(p.g * k); }  // :33-35
+// AngularFrequency (:33-35) = sqrt(g |k|) lives in wave_data (spectrum_math.h).
 
 __device__ __forceinline__ float tma_correction(const Sp& p, float w) {  // :38-43
     float wh = w * sqrtf(p.D / p.g);
@@ -79,22 +79,19 @@ __global__ __launch_bounds__(256) void k_init_spectrum(DevView v, Sp p) {
         const int tile = u / v.C, c = u - tile * v.C;
         const float* cs = v.casc + c * 5;
         const float2 g = v.noise[(size_t)tile * plane + t];
-        const int nx = x - n / 2, nz = y - n / 2;
         const float dk = 2.0f * kPi / cs[0];  // :110
-        const float kx = (float)nx * dk, kz = (float)nz * dk;
-        const float kmag = sqrtf(kx * kx + kz * kz);
-        float4 h, w;
-        if (kmag >= cs[1] && kmag <= cs[2]) {
-            const float kangle = atan2f(kz, kx);
-            const float om = angular_frequency(p, kmag);
+        float kmag;
+        const float4 w = wave_data(x, y, n, cs, p.g, &kmag);
+        float4 h;
+        if (kmag >= cs[1] && kmag <= cs[2]) {  // :114
+            const float kangle = atan2f(w.z, w.x);
+            const float om = w.w;  // angular_frequency(kmag) (:116), computed in wave_data
             const float amp = sqrtf(2.0f * tma_correction(p, om) * jonswap(p, om, wp) *
                                     directional_spread(p, om, wp, kangle, cs[3]) * short_waves_fade(kmag, cs[4]) *
                                     frequency_derivative(p, kmag, om) / kmag * dk * dk);
             h = make_float4(g.x / 2.0f * amp, g.y / 2.0f * amp, 0.0f, 0.0f);
-            w = make_float4(kx, 1.0f / kmag, kz, om);
         } else {
             h = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            w = make_float4(kx, 1.0f, kz, 0.0f);
         }
         v.h0[i] = h;
         v.waves[i] = w;
@@ -132,6 +129,15 @@ __global__ __launch_bounds__(256) void k_evolve(DevView v, float time) {
     }
 }
 
+// Index of texel i = (u, y, x) in the column-tile-major layout [u][x/W][y][W]
+// of the foam state (and of the fused path's intermediate planes).
+__device__ __forceinline__ size_t tiled_index(size_t i, int n, int w) {
+    const size_t plane = (size_t)n * n;
+    const size_t u = i / plane, t = i - u * plane;
+    const int y = (int)(t / n), x = (int)(t - (size_t)y * n);
+    return ((u * (n / w) + x / w) * n + y) * w + (x % w);
+}
+
 __global__ __launch_bounds__(256) void k_fill(DevView v) {
     const size_t total = (size_t)v.n * v.n * v.units;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
@@ -140,11 +146,20 @@ __global__ __launch_bounds__(256) void k_fill(DevView v) {
         if (v.planes == 4) {
             const float2 c = v.plane[2][i], d = v.plane[3][i];
             v.deriv[i] = make_float4(c.x, c.y, d.x, d.y);
-            const float foam = foam_update(v.turb[i].x, d.x, d.y, b.y);
+            const size_t fi = tiled_index(i, v.n, v.tile_w);
+            const float foam = foam_update(v.foam[fi], d.x, d.y, b.y);
+            v.foam[fi] = foam;
             v.turb[i] = make_float4(foam, foam, foam, foam);
             if (v.normals) v.normal[i] = normal_from_deriv(c.x, c.y, d.x, d.y);
         }
     }
+}
+
+// Foam state <- TURB.x (after an ocean_write of the TURB texture: resume).
+__global__ __launch_bounds__(256) void k_foam_import(DevView v) {
+    const size_t total = (size_t)v.n * v.n * v.units;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x)
+        v.foam[tiled_index(i, v.n, v.tile_w)] = v.turb[i].x;
 }
 
 unsigned grid_for(size_t total) {
@@ -167,6 +182,11 @@ hipError_t launch_conjugate(const DevView& v, hipStream_t s) {
 
 hipError_t launch_evolve(const DevView& v, float t, hipStream_t s) {
     hipLaunchKernelGGL(k_evolve, dim3(grid_for((size_t)v.n * v.n * v.units)), dim3(256), 0, s, v, t);
+    return hipGetLastError();
+}
+
+hipError_t launch_foam_import(const DevView& v, hipStream_t s) {
+    hipLaunchKernelGGL(k_foam_import, dim3(grid_for((size_t)v.n * v.n * v.units)), dim3(256), 0, s, v);
     return hipGetLastError();
 }
 
