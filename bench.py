@@ -28,6 +28,7 @@ import torch  # noqa: E402  (import before ocean_hip: one HIP runtime per proces
 import torch.distributed as dist  # noqa: E402
 
 import ocean_hip as oh  # noqa: E402
+from ocean_hip.shard import reduce_timing, shard_tiles, tile_seed  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md (chip-level parameters)
 
@@ -141,15 +142,18 @@ def main():
     cfg = CONFIGS[args.config]
     n, C = cfg["n"], cfg["cascades"]
     if cfg["per_rank"]:
-        tiles = cfg["tiles"]  # each rank runs its own ocean(s): weak scaling over independent oceans
+        # weak scaling: every rank runs its own ocean(s) (global tiles rank*T .. rank*T+T-1)
+        tiles = cfg["tiles"]
+        first = rank * tiles
     else:
-        tiles = cfg["tiles"] // world + (1 if rank < cfg["tiles"] % world else 0)
+        # the job's fixed batch of tiles split into contiguous blocks over the ranks
+        first, tiles = shard_tiles(cfg["tiles"], world, rank)
     flags = (oh.F_DISPLACEMENT_ONLY if cfg["disp_only"] else 0) | (oh.F_UNFUSED if args.unfused else 0)
 
     torch.cuda.set_device(local)
     ctx = oh.OceanContext(n, C, tiles, flags, device=local)
     ctx.set_params(SCENE_PARAMS, SCENE_CASCADES[:C])
-    ctx.generate_noise(20251121 + rank * max(tiles, 1))
+    ctx.generate_noise(tile_seed(20251121, first))
     ctx.init_spectrum()
     ctx.synchronize()
 
@@ -192,15 +196,8 @@ def main():
     kb_ms, kb_n = ctx.kernel_stats(1)
     ctx.set_kernel_timing(False)
 
-    if world > 1:
-        tt = torch.tensor([elapsed, elapsed_ev], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed, elapsed_ev = float(tt[0]), float(tt[1])
-        tot = torch.tensor([tiles], dtype=torch.float64)
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        total_tiles = int(tot[0])
-    else:
-        total_tiles = tiles
+    elapsed, total_tiles = reduce_timing(elapsed, tiles, world)
+    elapsed_ev, _ = reduce_timing(elapsed_ev, tiles, world)
 
     units = tiles * C
     B = algorithmic_bytes(n, units, cfg["disp_only"])
@@ -259,7 +256,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / args.steps, 5),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if cfg["per_rank"] else "strong",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (scene parameters of Waves.unity, seeded noise 20251121+tile)",

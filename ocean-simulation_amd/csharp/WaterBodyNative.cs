@@ -1,0 +1,102 @@
+// WaterBody-shaped facade over liboceanhip.so: the same public surface as
+// Assets/Scripts/Water/WaterBody.cs (fields :10-33, CalculateWavesTexturesAtTime
+// :180, GetWaterHeight :195, Awake :211, Update :284, OnDisable :300), with the
+// GPU work done by the MI355X library instead of ComputeShader.Dispatch.
+// Engine-free (no UnityEngine types) so it also runs in a plain .NET host; a
+// Unity MonoBehaviour can own one of these and forward its lifecycle calls.
+// Compile-ready; not built here (no C# toolchain in the build image).
+using System;
+
+namespace OceanHip
+{
+    public sealed class WaterCascadeDesc  // WaterCascade.cs:10-24
+    {
+        public float wavelength = 10.0f, cutoffHigh = 5.0f, cutoffLow = 0.0001f, swell = 0.4f, fade = 0.1f;
+    }
+
+    public sealed class WaterBodyNative : IDisposable
+    {
+        // Ocean parameters (WaterBody.cs:10-14) and texture size (:29)
+        public float windSpeed = 1.0f;
+        public float windDirectionX = 1.0f, windDirectionY = 1.0f;
+        public float gravity = 9.81f;
+        public float fetch = 1.0f;
+        public float depth = 4.0f;
+        public int texturesSize = 256;
+        public WaterCascadeDesc[] cascades = { new WaterCascadeDesc() };
+        public int device = 0;
+        public ulong seed = 20251121;   // the reference's UnityEngine.Random is unseeded; this library's generator is
+
+        IntPtr ctx = IntPtr.Zero;
+        float[] buoyancyData;           // displacement slice 0, RGBA fp32 [y][x] (WaterBody.cs:58, :295)
+
+        public void Awake()
+        {
+            OceanNative.Check(OceanNative.ocean_create(device, texturesSize, cascades.Length, 1, OceanFlags.None, out ctx),
+                              "ocean_create");
+            ApplyParams();
+            OceanNative.Check(OceanNative.ocean_generate_noise(ctx, seed), "ocean_generate_noise");
+            OceanNative.Check(OceanNative.ocean_init_spectrum(ctx), "ocean_init_spectrum");
+        }
+
+        void ApplyParams()
+        {
+            var p = new OceanParams { windSpeed = windSpeed, windDirX = windDirectionX, windDirY = windDirectionY,
+                                      gravity = gravity, fetch = fetch, depth = depth };
+            var cs = new OceanCascade[cascades.Length];
+            for (int i = 0; i < cascades.Length; i++)
+                cs[i] = new OceanCascade { wavelength = cascades[i].wavelength, cutoffLow = cascades[i].cutoffLow,
+                                           cutoffHigh = cascades[i].cutoffHigh, swell = cascades[i].swell,
+                                           fade = cascades[i].fade };
+            OceanNative.Check(OceanNative.ocean_set_params(ctx, ref p, cs), "ocean_set_params");
+        }
+
+        // The commented OnValidate of WaterBody.cs:324-337: parameter change -> spectrum re-init.
+        public void OnValidate()
+        {
+            if (ctx == IntPtr.Zero) return;
+            ApplyParams();
+            OceanNative.Check(OceanNative.ocean_init_spectrum(ctx), "ocean_init_spectrum");
+        }
+
+        public void CalculateWavesTexturesAtTime(float time) =>
+            OceanNative.Check(OceanNative.ocean_step(ctx, time), "ocean_step");
+
+        public void Update(float time)
+        {
+            CalculateWavesTexturesAtTime(time);
+            var buf = buoyancyData ?? new float[texturesSize * texturesSize * 4];
+            OceanNative.Check(OceanNative.ocean_read(ctx, OceanTexture.Displacement, 0, 0, buf,
+                                                     (UIntPtr)(buf.Length * sizeof(float))), "ocean_read");
+            buoyancyData = buf;
+        }
+
+        // WaterBody.cs:195-209, including the mapping over [-texturesSize/2, texturesSize/2].
+        public float GetWaterHeight(float worldX, float worldZ)
+        {
+            if (buoyancyData == null) return 0f;
+            float InverseLerp(float a, float b, float v) => a == b ? 0f : Math.Clamp((v - a) / (b - a), 0f, 1f);
+            float u = InverseLerp(-texturesSize / 2, texturesSize / 2, worldX);
+            float v = InverseLerp(-texturesSize / 2, texturesSize / 2, worldZ);
+            int x = Math.Clamp((int)(u * texturesSize), 0, texturesSize - 1);
+            int y = Math.Clamp((int)(v * texturesSize), 0, texturesSize - 1);
+            return buoyancyData[(y * texturesSize + x) * 4 + 1];  // .g = Dy
+        }
+
+        // Texture-out contract: device pointers for same-process renderers (WaterBody.cs:277-281).
+        public IntPtr DeviceTexture(OceanTexture tex, out ulong bytes)
+        {
+            OceanNative.Check(OceanNative.ocean_get_device_ptr(ctx, tex, out var p, out var b), "ocean_get_device_ptr");
+            bytes = (ulong)b;
+            return p;
+        }
+
+        public void OnDisable() => Dispose();
+
+        public void Dispose()
+        {
+            if (ctx != IntPtr.Zero) OceanNative.ocean_destroy(ctx);
+            ctx = IntPtr.Zero;
+        }
+    }
+}

@@ -1,0 +1,63 @@
+"""Multi-process (world_size 2, gloo, CPU) tests of the sharding used by bench.py
+for BASELINE cfg4 (256 independent tiles over the GPUs of one node).  The data
+path has no collective: only the barrier, max-elapsed and
+tile-count reductions run over torch.distributed."""
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+from ocean_hip.shard import reduce_timing, shard_tiles, tile_seed
+
+
+@pytest.mark.parametrize("total,world", [(256, 8), (256, 2), (7, 3), (3, 4), (1, 1)])
+def test_shards_cover_every_tile_once(total, world):
+    seen = []
+    for r in range(world):
+        first, count = shard_tiles(total, world, r)
+        seen.extend(range(first, first + count))
+    assert seen == list(range(total))
+    counts = [shard_tiles(total, world, r)[1] for r in range(world)]
+    assert max(counts) - min(counts) <= 1
+
+
+def test_tile_seed_is_global():
+    # rank 1 of 2 over 256 tiles starts at global tile 128: seed 20251121 + 128
+    first, _ = shard_tiles(256, 2, 1)
+    assert tile_seed(20251121, first) == 20251121 + 128
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    first, tiles = shard_tiles(256, world, rank)
+    dist.barrier()
+    elapsed, total = reduce_timing(0.5 + rank, tiles, world)
+    q.put((rank, first, tiles, elapsed, total))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_barrier_and_reductions():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [o[1:3] for o in out] == [(0, 128), (128, 128)]
+    for o in out:
+        assert o[3] == 1.5 and o[4] == 256  # max elapsed, summed tiles on every rank
