@@ -29,7 +29,8 @@ namespace {
 
 constexpr int pa3_rows(int N, int RS = 2) { return N >= 1024 * RS ? 1 : 1024 * RS / N; }
 
-template <int N, int P, int RS = 1, bool READW = false, bool PF = false, int WPS = 0>
+template <int N, int P, int RS = 1, bool READW = false, bool PF = false, int WPS = 0, int SMODE = 0,
+          bool GTW = false>
 __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems, WPS) void k_pass_a3(DevView v, float time,
                                                                                    int total_rows) {
     constexpr int RB = pa3_rows(N, RS);
@@ -44,9 +45,10 @@ __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems, WPS) void k_pass_
     constexpr int NSL = N / E::RL;        // last-stage Ns
     static_assert(T / NJ == RB, "stage-0 mapping: lane -> (row, j), butterfly m -> plane m");
     __shared__ float2 lds[E::LDS_ELEMS];
-    __shared__ float2 twl[TW::kLdsEntries];
-    TW::load(twl, v.tw, threadIdx.x, T);
-    const float2* tws = TW::table(twl, v.tw);
+    // twiddles: LDS copy, or (GTW) read straight from the L1/L2-resident global table
+    __shared__ float2 twl[GTW ? 1 : TW::kLdsEntries];
+    if constexpr (!GTW) TW::load(twl, v.tw, threadIdx.x, T);
+    const float2* tws = GTW ? TW::global_table(v.tw) : TW::table(twl, v.tw);
     const int rr = (int)threadIdx.x / NJ, j = (int)threadIdx.x % NJ;  // stage-0 lane coordinates
     const int items = (total_rows + RB - 1) / RB;
 
@@ -91,6 +93,14 @@ __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems, WPS) void k_pass_
             E::template bj<E::RL>((int)threadIdx.x + m * T, b, jj);
             const int p = b / RB, r2 = b % RB;
             const int row2 = item * RB + r2;
+            if constexpr (SMODE == 2) {  // timing experiment: no stores
+                asm volatile("" ::"v"(val.x), "v"(val.y));
+                return;
+            }
+            if constexpr (SMODE == 1) {  // timing experiment: row-major stores (wrong layout for pass B)
+                if (row2 < total_rows) v.tplane[(size_t)p * v.plane_stride + (size_t)row2 * N + jj + q * NSL] = val;
+                return;
+            }
             if (row2 < total_rows) {
                 const int u2 = row2 / N, y2 = row2 % N;
                 float2* rowp = v.tplane + (size_t)p * v.plane_stride + ((size_t)u2 * TILES * N + y2) * W;
@@ -230,14 +240,15 @@ int grid3(K kernel, int threads, int items) {
     return items < g ? items : g;
 }
 
-template <int N, int P, int RS = 1, bool READW = false, bool PF = false, int WPS = 0>
+template <int N, int P, int RS = 1, bool READW = false, bool PF = false, int WPS = 0, int SMODE = 0,
+          bool GTW = false>
 hipError_t go_a3k(const DevView& v, float t, hipStream_t s) {
     constexpr int RB = pa3_rows(N, RS);
     constexpr int T = RB * P * N / kElems;
     const int total = v.units * N;
     const int items = (total + RB - 1) / RB;
-    const int g = grid3(k_pass_a3<N, P, RS, READW, PF, WPS>, T, items);
-    hipLaunchKernelGGL((k_pass_a3<N, P, RS, READW, PF, WPS>), dim3(g), dim3(T), 0, s, v, t, total);
+    const int g = grid3(k_pass_a3<N, P, RS, READW, PF, WPS, SMODE, GTW>, T, items);
+    hipLaunchKernelGGL((k_pass_a3<N, P, RS, READW, PF, WPS, SMODE, GTW>), dim3(g), dim3(T), 0, s, v, t, total);
     return hipGetLastError();
 }
 
@@ -259,6 +270,12 @@ hipError_t go_a3(const DevView& v, float t, hipStream_t s) {
             case 2: return go_a3k<N, P, 2, true, true>(v, t, s);    // + wave data read, not recomputed
             case 3: return go_a3k<N, P, 1, false, true>(v, t, s);   // prefetch
             case 4: return go_a3k<N, P, 1, true, false>(v, t, s);   // wave data read
+            case 10: return go_a3k<N, P, 1, false, false, 0, 1>(v, t, s);  // timing only: row-major stores
+            case 11: return go_a3k<N, P, 1, false, false, 0, 2>(v, t, s);  // timing only: no stores
+            case 12: return go_a3k<N, P, 2, false, false, 0, 1>(v, t, s);  // timing only: RB=2 row-major
+            case 5: return go_a3k<N, P, 1, false, false, 0, 0, true>(v, t, s);  // global twiddles (4 WG/CU)
+            case 6: return go_a3k<N, P, 1, false, false, 4, 0, true>(v, t, s);  // + <=128 VGPR
+            case 13: return go_a3k<N, P, 1, false, false, 0, 2, true>(v, t, s);  // timing: no stores, global tw
             default: break;
         }
     }

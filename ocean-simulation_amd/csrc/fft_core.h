@@ -28,8 +28,12 @@ constexpr int col_tile(int N) { return (8192 / N) < 4 ? 4 : ((8192 / N) > N ? N 
 
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+// Complex multiply with fused multiply-adds (the FFT is not bound to the
+// reference's rounding sequence: its parity is a norm-relative tolerance, and
+// FMA is the more accurate form; the evolve / wave-data code that IS bit-exact
+// lives in spectrum_math.h and is built without contraction).
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+    return make_float2(fmaf(a.x, b.x, -(a.y * b.y)), fmaf(a.x, b.y, a.y * b.x));
 }
 __device__ __forceinline__ float2 cmul_i(float2 a) { return make_float2(-a.y, a.x); }  // i * a
 

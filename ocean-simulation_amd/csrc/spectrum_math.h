@@ -31,11 +31,37 @@ __device__ __forceinline__ float4 wave_data(int x, int y, int n, const float* cs
     return make_float4(kx, 1.0f, kz, 0.0f);
 }
 
+// sin and cos of an fp32 argument, |x| < 2^17 on the fast path: Cody-Waite
+// reduction by pi/2 with a three-part FMA split (exact products), then
+// minimax polynomials on [-pi/4, pi/4] (Cephes sinf/cosf coefficients);
+// max error ~1-2 ulp against correctly rounded sin/cos.  Larger |x| falls back
+// to the library sincosf.  ~25 VALU instead of the library's ~45 plus its
+// Payne-Hanek branch.
+__device__ __forceinline__ void sincos_fast(float x, float* s, float* c) {
+    if (!(fabsf(x) < 131072.0f)) {
+        sincosf(x, s, c);
+        return;
+    }
+    const float n = rintf(x * 0.636619772367581343f);
+    float r = fmaf(-n, 1.57079637050628662109375f, x);
+    r = fmaf(-n, -4.37113882867379e-08f, r);
+    r = fmaf(-n, -1.7151245e-15f, r);
+    const float r2 = r * r;
+    const float sp = fmaf(fmaf(fmaf(-1.9515295891e-4f, r2, 8.3321608736e-3f), r2, -1.6666654611e-1f), r2 * r, r);
+    const float cp = fmaf(fmaf(fmaf(2.443315711809948e-5f, r2, -1.388731625493765e-3f), r2, 4.166664568298827e-2f),
+                          r2 * r2, fmaf(-0.5f, r2, 1.0f));
+    const int q = (int)n & 3;
+    const float ss = (q & 1) ? cp : sp, cc = (q & 1) ? sp : cp;
+    *s = (q & 2) ? -ss : ss;
+    *c = ((q + 1) & 2) ? -cc : cc;
+}
+
 // TimeDependentSpectrum.compute:20-47 for one texel-cascade.
 __device__ __forceinline__ Planes4 evolve_texel(float4 h, float4 w, float t) {
     Planes4 o;
     float phase = w.w * t;
-    float ex = cosf(phase), ey = sinf(phase);
+    float ex, ey;
+    sincos_fast(phase, &ey, &ex);
     // ComplexMult(h0.xy, e) + ComplexMult(h0.zw, conj(e))  (:26)
     float hx = (h.x * ex - h.y * ey) + (h.z * ex - h.w * (-ey));
     float hy = (h.x * ey + h.y * ex) + (h.z * (-ey) + h.w * ex);
