@@ -30,13 +30,13 @@ namespace {
 constexpr int pa3_rows(int N, int RS = 2) { return N >= 1024 * RS ? 1 : 1024 * RS / N; }
 
 template <int N, int P, int RS = 1, bool READW = false, bool PF = false, int WPS = 0, int SMODE = 0,
-          bool GTW = false>
+          bool GTW = false, bool PAIR = false, bool CTW = false, bool DEF = false>
 __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems, WPS) void k_pass_a3(DevView v, float time,
-                                                                                   int total_rows) {
+                                                                                   int total_rows, int xcd_remap) {
     constexpr int RB = pa3_rows(N, RS);
     constexpr int FIRST = 16 / P;
-    using E = Engine<N, RB * P, false, true, FIRST>;
-    using TW = StageTw<N, FIRST>;
+    using TW = std::conditional_t<CTW, StageTwCompact<N, FIRST>, StageTw<N, FIRST>>;
+    using E = Engine<N, RB * P, false, true, FIRST, TW>;
     constexpr int T = E::THREADS;
     constexpr int R0 = E::R0;             // = FIRST (texels per lane)
     constexpr int NJ = N / R0;            // stage-0 butterflies per sequence
@@ -48,7 +48,13 @@ __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems, WPS) void k_pass_
     // twiddles: LDS copy, or (GTW) read straight from the L1/L2-resident global table
     __shared__ float2 twl[GTW ? 1 : TW::kLdsEntries];
     if constexpr (!GTW) TW::load(twl, v.tw, threadIdx.x, T);
-    const float2* tws = GTW ? TW::global_table(v.tw) : TW::table(twl, v.tw);
+    const float2* tws;
+    if constexpr (GTW) tws = StageTw<N, FIRST>::global_table(v.tw);
+    else tws = TW::table(twl, v.tw);
+    // per-cascade band constants in LDS: a vector load here would be waited on
+    // with vmcnt(0) together with the previous item's stores and the prefetch
+    __shared__ WaveBand band[kMaxCascades];
+    if ((int)threadIdx.x < v.C) band[threadIdx.x] = wave_band(v.casc + threadIdx.x * 5);
     const int rr = (int)threadIdx.x / NJ, j = (int)threadIdx.x % NJ;  // stage-0 lane coordinates
     const int items = (total_rows + RB - 1) / RB;
 
@@ -65,27 +71,48 @@ __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems, WPS) void k_pass_
             for (int r = 0; r < R0; ++r) ww[r] = bload4(w2, (rr * N + j) * 16, r * NJ * 16);
         }
     };
-    int item = blockIdx.x;
+    // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs, so
+    // blockIdx b runs on XCD b % 8.  Give each XCD a contiguous run of rows:
+    // rows y and y+1 share every 128-B line of the tile-major intermediate
+    // (64 B each), and the XCD's L2 then merges the halves into whole-line
+    // write-backs instead of two partial writes from two L2s.
+    const int g = (int)gridDim.x;
+    const int slot = (xcd_remap && g % 8 == 0) ? ((int)blockIdx.x % 8) * (g / 8) + (int)blockIdx.x / 8
+                                                 : (int)blockIdx.x;
+    int item = slot;
     if (item < items) load(item, h, wv);
+    // DEF: the previous item's outputs are stored during this item's evolve
+    // (4 per texel) instead of in one burst after the last stage.
+    constexpr bool kDef = DEF && (kElems / E::RL == 1) && (NSL % W == 0);
+    float2 pend[kDef ? kElems : 1];
+    float2* pdst = nullptr;  // lane's first output texel of the pending item (null: none / past end)
+    bool have_pend = false;
+    auto store_pend = [&](int q) { pdst[(size_t)q * (NSL / W) * N * W] = pend[q]; };
     __syncthreads();  // twiddles
-    for (; item < items; item += gridDim.x) {
-        const int next = item + gridDim.x;
+    for (; item < items; item += g) {
+        const int next = item + g;
         if constexpr (PF) {
             if (next < items) load(next, hn, wvn);
         }
         // stage-0 inputs: plane m of texel x = j + r*NJ of row (item*RB + rr)
         const int row = item * RB + rr;
         const int u = row / N, y = row % N;
-        const float* cs = v.casc + (u % v.C) * 5;
+        const WaveBand wb = band[(v.casc0 + u) % v.C];
         float2 in[kElems];
 #pragma unroll
         for (int r = 0; r < R0; ++r) {
             float4 wd;
             if constexpr (READW) wd = wv[r];
-            else wd = wave_data(j + r * NJ, y, N, cs, v.gravity);
+            else wd = wave_data(j + r * NJ, y, N, wb, v.gravity);
             const Planes4 o = evolve_texel(h[r], wd, time);
 #pragma unroll
             for (int m = 0; m < P; ++m) in[m * R0 + r] = o.p[m];
+            if constexpr (kDef) {
+                if (have_pend && pdst) {
+#pragma unroll
+                    for (int q = r * (kElems / R0); q < (r + 1) * (kElems / R0); ++q) store_pend(q);
+                }
+            }
         }
         // outputs: sequence b = p*RB + rr', element x -> tplane[p][u'][x/W][y'][x%W]
         auto emit = [&](int m, int q, float2 val) {
@@ -95,6 +122,18 @@ __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems, WPS) void k_pass_
             const int row2 = item * RB + r2;
             if constexpr (SMODE == 2) {  // timing experiment: no stores
                 asm volatile("" ::"v"(val.x), "v"(val.y));
+                return;
+            }
+            if constexpr (kDef) {
+                if (q == 0) {
+                    pdst = nullptr;
+                    if (row2 < total_rows) {
+                        const int u2 = row2 / N, y2 = row2 % N;
+                        pdst = v.tplane + (size_t)p * v.plane_stride + ((size_t)u2 * TILES * N + y2) * W +
+                               (size_t)(jj / W) * N * W + (jj % W);
+                    }
+                }
+                pend[q] = val;
                 return;
             }
             if constexpr (SMODE == 1) {  // timing experiment: row-major stores (wrong layout for pass B)
@@ -114,7 +153,26 @@ __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems, WPS) void k_pass_
                 }
             }
         };
-        E::run_regs(in, lds, tws, emit);
+        // PAIR: lane pairs swap so each lane stores 16 B (two consecutive x of one row)
+        auto emit_pair = [&](int m, int q, float4 xy) {
+            int b, jj;
+            E::template bj<E::RL>((int)threadIdx.x + m * T, b, jj);
+            const int p = b / RB, r2 = b % RB;
+            const int row2 = item * RB + r2;
+            if (row2 < total_rows) {
+                const int u2 = row2 / N, y2 = row2 % N;
+                const int x = (jj & ~1) + q * NSL;
+                float2* rowp = v.tplane + (size_t)p * v.plane_stride + ((size_t)u2 * TILES * N + y2) * W;
+                *reinterpret_cast<float4*>(rowp + (size_t)(x / W) * N * W + (x % W)) = xy;
+            }
+        };
+        if constexpr (PAIR) {
+            PairEmit<decltype(emit_pair)> pe{emit_pair};
+            E::run_regs(in, lds, tws, pe);
+        } else {
+            E::run_regs(in, lds, tws, emit);
+        }
+        have_pend = true;
         if constexpr (PF) {
 #pragma unroll
             for (int r = 0; r < R0; ++r) {
@@ -127,11 +185,17 @@ __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems, WPS) void k_pass_
             if (next < items) load(next, h, wv);
         }
     }
+    if constexpr (kDef) {
+        if (have_pend && pdst) {
+#pragma unroll
+            for (int q = 0; q < kElems; ++q) store_pend(q);
+        }
+    }
 }
 
 // Pass B: one item = (unit, W-column tile); planes in the order DyDxz, DxDz,
 // DxxDzz, DyxDyz with the next plane prefetched into registers.
-template <int N, int P>
+template <int N, int P, bool KEEPREG = false, int PFD = 1>
 __global__ __launch_bounds__(col_tile(N) * N / kElems) void k_pass_b3(DevView v, int items) {
     using CT = ColTile<N>;
     using E = typename CT::E;
@@ -140,7 +204,7 @@ __global__ __launch_bounds__(col_tile(N) * N / kElems) void k_pass_b3(DevView v,
     constexpr int T = CT::T;
     constexpr int RL = CT::RL;
     constexpr int TILE = W * N;
-    constexpr bool kKeepLds = (E::LDS_ELEMS + TW::kLdsEntries + kElems * T) * 8 <= 160 * 1024;
+    constexpr bool kKeepLds = !KEEPREG && (E::LDS_ELEMS + TW::kLdsEntries + kElems * T) * 8 <= 160 * 1024;
     __shared__ float2 lds[E::LDS_ELEMS];
     __shared__ float2 twl[TW::kLdsEntries];
     __shared__ float2 keep_lds[kKeepLds ? kElems * T : 1];
@@ -170,9 +234,13 @@ __global__ __launch_bounds__(col_tile(N) * N / kElems) void k_pass_b3(DevView v,
         for (int i = 0; i < kElems; ++i) d[i] = bload2(w, toff * 8, CT::in_dy(i) * W * 8);
     };
 
-    float2 cur[kElems], nxt[kElems];
+    // PFD planes in flight ahead of the one being transformed (register ring)
+    float2 cur[kElems], nxt[kElems], nx2[PFD > 1 ? kElems : 1];
     int item = blockIdx.x;
-    if (item < items) load(item, order[0], cur);
+    if (item < items) {
+        load(item, order[0], cur);
+        if constexpr (PFD > 1) load(item, order[1], nxt);
+    }
     __syncthreads();
     for (; item < items; item += gridDim.x) {
         const int x0 = (item % CT::tiles) * W;
@@ -180,8 +248,13 @@ __global__ __launch_bounds__(col_tile(N) * N / kElems) void k_pass_b3(DevView v,
 #pragma unroll
         for (int pi = 0; pi < P; ++pi) {
             const int p = order[pi];
-            if (pi + 1 < P) load(item, order[pi + 1], nxt);
-            else if (item + (int)gridDim.x < items) load(item + gridDim.x, order[0], nxt);
+            if constexpr (PFD > 1) {
+                if (pi + 2 < P) load(item, order[pi + 2], nx2);
+                else if (item + (int)gridDim.x < items) load(item + gridDim.x, order[pi + 2 - P], nx2);
+            } else {
+                if (pi + 1 < P) load(item, order[pi + 1], nxt);
+                else if (item + (int)gridDim.x < items) load(item + gridDim.x, order[0], nxt);
+            }
             float fb[kElems];
             if (p == 3) {
                 const Win rf = make_win(v.foam + (size_t)item * TILE, TILE * 4);
@@ -214,10 +287,18 @@ __global__ __launch_bounds__(col_tile(N) * N / kElems) void k_pass_b3(DevView v,
             };
             E::run_regs(cur, lds, tws, emit);
 #pragma unroll
-            for (int i = 0; i < kElems; ++i) cur[i] = nxt[i];
+            for (int i = 0; i < kElems; ++i) {
+                cur[i] = nxt[i];
+                if constexpr (PFD > 1) nxt[i] = nx2[i];
+            }
             __syncthreads();
         }
     }
+}
+
+int env_int(const char* name, int dflt) {
+    const char* e = std::getenv(name);
+    return e ? std::atoi(e) : dflt;
 }
 
 int num_cus3() {
@@ -241,14 +322,21 @@ int grid3(K kernel, int threads, int items) {
 }
 
 template <int N, int P, int RS = 1, bool READW = false, bool PF = false, int WPS = 0, int SMODE = 0,
-          bool GTW = false>
+          bool GTW = false, bool PAIR = false, bool CTW = false, bool DEF = false>
 hipError_t go_a3k(const DevView& v, float t, hipStream_t s) {
     constexpr int RB = pa3_rows(N, RS);
     constexpr int T = RB * P * N / kElems;
     const int total = v.units * N;
     const int items = (total + RB - 1) / RB;
-    const int g = grid3(k_pass_a3<N, P, RS, READW, PF, WPS, SMODE, GTW>, T, items);
-    hipLaunchKernelGGL((k_pass_a3<N, P, RS, READW, PF, WPS, SMODE, GTW>), dim3(g), dim3(T), 0, s, v, t, total);
+    int g = grid3(k_pass_a3<N, P, RS, READW, PF, WPS, SMODE, GTW, PAIR, CTW, DEF>, T, items);
+    static const int cap = env_int("OCEAN_A3_GRID", 0);
+    if (cap > 0 && g > cap) g = cap;
+    static const int remap = [] {
+        const char* e = std::getenv("OCEAN_XCD_REMAP");
+        return e ? std::atoi(e) : 0;
+    }();
+    hipLaunchKernelGGL((k_pass_a3<N, P, RS, READW, PF, WPS, SMODE, GTW, PAIR, CTW, DEF>), dim3(g), dim3(T), 0, s, v, t,
+                       total, remap);
     return hipGetLastError();
 }
 
@@ -275,6 +363,13 @@ hipError_t go_a3(const DevView& v, float t, hipStream_t s) {
             case 12: return go_a3k<N, P, 2, false, false, 0, 1>(v, t, s);  // timing only: RB=2 row-major
             case 5: return go_a3k<N, P, 1, false, false, 0, 0, true>(v, t, s);  // global twiddles (4 WG/CU)
             case 6: return go_a3k<N, P, 1, false, false, 4, 0, true>(v, t, s);  // + <=128 VGPR
+            case 7: return go_a3k<N, P, 1, false, true, 0, 0, false, true>(v, t, s);  // prefetch + paired 16 B stores
+            case 8: return go_a3k<N, P, 1, false, false, 0, 0, false, true>(v, t, s);  // paired 16 B stores
+            case 9: return go_a3k<N, P, 1, false, true, 0, 0, false, false, true>(v, t, s);  // prefetch + compact tw
+            case 14: return go_a3k<N, P, 1, false, true, 0, 2, false, false, true>(v, t, s);  // timing: 9, no stores
+            case 15: return go_a3k<N, P, 1, false, true, 0, 0, false, false, false, true>(v, t, s);  // PF + deferred stores
+            case 16: return go_a3k<N, P, 1, false, false, 0, 0, false, false, false, true>(v, t, s);  // deferred stores
+            case 17: return go_a3k<N, P, 1, false, true, 0, 0, false, false, true, true>(v, t, s);  // PF+DEF+compact tw
             case 13: return go_a3k<N, P, 1, false, false, 0, 2, true>(v, t, s);  // timing: no stores, global tw
             default: break;
         }
@@ -282,14 +377,29 @@ hipError_t go_a3(const DevView& v, float t, hipStream_t s) {
     return go_a3k<N, P>(v, t, s);
 }
 
-template <int N, int P>
-hipError_t go_b3(const DevView& v, hipStream_t s) {
+template <int N, int P, bool KEEPREG, int PFD>
+hipError_t go_b3k(const DevView& v, hipStream_t s) {
     constexpr int W = col_tile(N);
     constexpr int T = W * N / kElems;
     const int items = v.units * (N / W);
-    const int g = grid3(k_pass_b3<N, P>, T, items);
-    hipLaunchKernelGGL((k_pass_b3<N, P>), dim3(g), dim3(T), 0, s, v, items);
+    int g = grid3(k_pass_b3<N, P, KEEPREG, PFD>, T, items);
+    static const int cap = env_int("OCEAN_B3_GRID", 0);
+    if (cap > 0 && g > cap) g = cap;
+    hipLaunchKernelGGL((k_pass_b3<N, P, KEEPREG, PFD>), dim3(g), dim3(T), 0, s, v, items);
     return hipGetLastError();
+}
+
+template <int N, int P>
+hipError_t go_b3(const DevView& v, hipStream_t s) {
+    static const int mode = env_int("OCEAN_B3_MODE", 0);
+    if constexpr (N == 1024) {
+        switch (mode) {
+            case 1: return go_b3k<N, P, true, 1>(v, s);   // keep values in registers
+            case 2: return go_b3k<N, P, false, 2>(v, s);  // two planes in flight
+            case 3: return go_b3k<N, P, true, 2>(v, s);   // both
+        }
+    }
+    return go_b3k<N, P, false, 1>(v, s);
 }
 
 }  // namespace

@@ -9,6 +9,9 @@
 
 namespace ocean {
 
+constexpr int kMaxCascades = 5;  // the consumer shader caps cascades at 5 (Water.shader:139)
+
+
 // Device-side view of one context: every texture of every (tile, cascade) unit.
 // unit u = tile * C + cascade; each texture is [u][y][x] (see include/ocean/ocean.h).
 struct DevView {
@@ -35,6 +38,7 @@ struct DevView {
     int tile_w;           // column-tile width W = col_tile(N) of the tile-major layouts below
     float2* tplane;       // fused intermediate, P planes x [U][N/W][N][W] (tile-major), stride plane_stride
     float* foam;          // foam state, [U][N/W][N][W] (tile-major); TURB is its broadcast RGBA image
+    int casc0;            // cascade of unit 0 of this view (sub-views over a unit range: u0 % C)
 };
 
 struct SpectrumParams {

@@ -81,7 +81,7 @@ __global__ __launch_bounds__(256) void k_init_spectrum(DevView v, Sp p) {
         const float2 g = v.noise[(size_t)tile * plane + t];
         const float dk = 2.0f * kPi / cs[0];  // :110
         float kmag;
-        const float4 w = wave_data(x, y, n, cs, p.g, &kmag);
+        const float4 w = wave_data(x, y, n, wave_band(cs), p.g, &kmag);
         float4 h;
         if (kmag >= cs[1] && kmag <= cs[2]) {  // :114
             const float kangle = atan2f(w.z, w.x);

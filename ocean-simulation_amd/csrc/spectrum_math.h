@@ -17,17 +17,25 @@ struct Planes4 {
 };
 
 // Wave data of texel (x, y) of a cascade (InitialSpectrum.compute:101-126):
-// k = (nx, nz) * 2 pi / L; in band: (kx, 1/|k|, kz, omega = sqrt(g |k|)),
-// else (kx, 1, kz, 0).  `cs` = {L, cutoff_low, cutoff_high, ...}.  Used by the
-// init kernel AND recomputed per frame by the fused row pass, so both see
-// bit-identical values (only correctly rounded + - * / sqrt).
-__device__ __forceinline__ float4 wave_data(int x, int y, int n, const float* cs, float g, float* kmag_out = nullptr) {
+// k = (nx, nz) * dk, dk = 2 pi / L; in band [lo, hi]: (kx, 1/|k|, kz,
+// omega = sqrt(g |k|)), else (kx, 1, kz, 0).  Used by the init kernel AND
+// recomputed per frame by the fused row pass, so both see bit-identical values
+// (only correctly rounded + - * / sqrt).
+struct WaveBand {
+    float dk, lo, hi;
+};
+
+// `cs` = {L, cutoff_low, cutoff_high, ...} (ocean_cascade order).
+__device__ __forceinline__ WaveBand wave_band(const float* cs) {
+    return WaveBand{2.0f * kPi / cs[0], cs[1], cs[2]};  // :110
+}
+
+__device__ __forceinline__ float4 wave_data(int x, int y, int n, WaveBand b, float g, float* kmag_out = nullptr) {
     const int nx = x - n / 2, nz = y - n / 2;
-    const float dk = 2.0f * kPi / cs[0];  // :110
-    const float kx = (float)nx * dk, kz = (float)nz * dk;
+    const float kx = (float)nx * b.dk, kz = (float)nz * b.dk;
     const float kmag = sqrtf(kx * kx + kz * kz);
     if (kmag_out) *kmag_out = kmag;
-    if (kmag >= cs[1] && kmag <= cs[2]) return make_float4(kx, 1.0f / kmag, kz, sqrtf(g * kmag));
+    if (kmag >= b.lo && kmag <= b.hi) return make_float4(kx, 1.0f / kmag, kz, sqrtf(g * kmag));
     return make_float4(kx, 1.0f, kz, 0.0f);
 }
 

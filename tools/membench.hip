@@ -66,6 +66,47 @@ __global__ void k_rowtile(const float2* __restrict__ a, float2* __restrict__ b) 
     for (int r = 0; r < 16; ++r) dst[r * 64] = v[r];
 }
 
+// 5. pass-A write shape: one row x 4 planes per 256-lane WG, wave = plane,
+//    lane jj writes x = jj + 64 q.  MODE 0: tile-major [x/8][y][8] float2;
+//    1: row-major float2; 2: tile-major, lane pairs as float4 (x even);
+//    3: tile-major with two rows per WG (rows y, y+1 -> 128 B lines whole).
+template <int MODE>
+__global__ void k_wr_a(float2* __restrict__ t, size_t plane_stride, int rows) {
+    const int p = threadIdx.x / 64, jj = threadIdx.x % 64;
+    if (MODE == 3) {
+        for (int row = blockIdx.x * 2; row < rows; row += gridDim.x * 2) {
+            const int u = row / N, y = row % N;
+            float2* base = t + p * plane_stride + (size_t)u * N * N + (size_t)y * 8;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                // lanes 0-7: row y cols 0-7 of tile, lanes 8-15 row y+1; 4 tiles per 16-lane group
+                const int l = jj, r = (l >> 3) & 1, col = l & 7, tl = (l >> 4) + 4 * q;
+                base[(size_t)tl * N * 8 + r * 8 + col] = make_float2(q, l);
+                base[(size_t)(tl + 64) * N * 8 + r * 8 + col] = make_float2(q, -l);
+            }
+        }
+        return;
+    }
+    for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+        const int u = row / N, y = row % N;
+        float2* pl = t + p * plane_stride;
+        if (MODE == 2) {
+#pragma unroll
+            for (int q = 0; q < 16; q += 2) {
+                const int x = (jj & ~1) + (q + (jj & 1)) * 64;
+                *(float4*)(pl + (size_t)u * N * N + (size_t)(x / 8) * N * 8 + y * 8 + x % 8) = make_float4(q, jj, 1, 2);
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int x = jj + q * 64;
+                const size_t o = MODE == 1 ? (size_t)row * N + x : (size_t)u * N * N + (size_t)(x / 8) * N * 8 + y * 8 + x % 8;
+                pl[o] = make_float2(q, jj);
+            }
+        }
+    }
+}
+
 template <class F>
 float timeit(F f, int reps) {
     hipEvent_t a, b;
@@ -121,6 +162,22 @@ int main() {
     {
         float ms = timeit([&] { hipLaunchKernelGGL(k_coltile_store4<16>, dim3(units * N / 16), dim3(1024), 0, 0, c, N / 16); }, reps);
         printf("col tile W=16 store f4 %8.1f GB/s  (%.1f us)\n", 1.0 * elems * 16 / ms / 1e6, ms * 1e3);
+    }
+    {
+        const int rows = 4 * N;  // 4 units (cfg3), 4 planes: 128 MiB written
+        const size_t ps = (size_t)rows * N;
+        const char* names[4] = {"passA tiled f2", "passA rowmajor f2", "passA tiled f4 pairs", "passA tiled 2 rows"};
+        for (int mode = 0; mode < 4; ++mode)
+            for (int grid : {768, 1024, 4096}) {
+                auto f = [&] {
+                    if (mode == 0) hipLaunchKernelGGL(k_wr_a<0>, dim3(grid), dim3(256), 0, 0, a, ps, rows);
+                    if (mode == 1) hipLaunchKernelGGL(k_wr_a<1>, dim3(grid), dim3(256), 0, 0, a, ps, rows);
+                    if (mode == 2) hipLaunchKernelGGL(k_wr_a<2>, dim3(grid), dim3(256), 0, 0, a, ps, rows);
+                    if (mode == 3) hipLaunchKernelGGL(k_wr_a<3>, dim3(grid / 2), dim3(256), 0, 0, a, ps, rows);
+                };
+                float ms = timeit(f, reps);
+                printf("%-22s grid %5d %8.1f GB/s  (%.1f us)\n", names[mode], grid, 4.0 * ps * 8 / ms / 1e6, ms * 1e3);
+            }
     }
     return 0;
 }
