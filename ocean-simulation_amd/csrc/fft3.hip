@@ -29,14 +29,16 @@ namespace {
 
 constexpr int pa3_rows(int N, int RS = 2) { return N >= 1024 * RS ? 1 : 1024 * RS / N; }
 
-template <int N, int P, int RS = 1, bool READW = false, bool PF = false, int WPS = 0, int SMODE = 0,
-          bool GTW = false, bool PAIR = false, bool CTW = false, bool DEF = false>
-__global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems, WPS) void k_pass_a3(DevView v, float time,
-                                                                                   int total_rows, int xcd_remap) {
+// RS: row-sets per workgroup (RB = pa3_rows(N, RS) rows); PF: prefetch the
+// next item's h0 before this item's transform (its loads are then ahead of
+// this item's stores in the in-order vmcnt queue, so waiting for them never
+// waits for the stores); NOSTORE: timing experiment only (no output).
+template <int N, int P, int RS, bool PF, bool NOSTORE = false>
+__global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems) void k_pass_a3(DevView v, float time, int total_rows) {
     constexpr int RB = pa3_rows(N, RS);
     constexpr int FIRST = 16 / P;
-    using TW = std::conditional_t<CTW, StageTwCompact<N, FIRST>, StageTw<N, FIRST>>;
-    using E = Engine<N, RB * P, false, true, FIRST, TW>;
+    using TW = StageTw<N, FIRST>;
+    using E = Engine<N, RB * P, false, true, FIRST>;
     constexpr int T = E::THREADS;
     constexpr int R0 = E::R0;             // = FIRST (texels per lane)
     constexpr int NJ = N / R0;            // stage-0 butterflies per sequence
@@ -45,12 +47,9 @@ __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems, WPS) void k_pass_
     constexpr int NSL = N / E::RL;        // last-stage Ns
     static_assert(T / NJ == RB, "stage-0 mapping: lane -> (row, j), butterfly m -> plane m");
     __shared__ float2 lds[E::LDS_ELEMS];
-    // twiddles: LDS copy, or (GTW) read straight from the L1/L2-resident global table
-    __shared__ float2 twl[GTW ? 1 : TW::kLdsEntries];
-    if constexpr (!GTW) TW::load(twl, v.tw, threadIdx.x, T);
-    const float2* tws;
-    if constexpr (GTW) tws = StageTw<N, FIRST>::global_table(v.tw);
-    else tws = TW::table(twl, v.tw);
+    __shared__ float2 twl[TW::kLdsEntries];
+    TW::load(twl, v.tw, threadIdx.x, T);
+    const float2* tws = TW::table(twl, v.tw);
     // per-cascade band constants in LDS: a vector load here would be waited on
     // with vmcnt(0) together with the previous item's stores and the prefetch
     __shared__ WaveBand band[kMaxCascades];
@@ -58,88 +57,42 @@ __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems, WPS) void k_pass_
     const int rr = (int)threadIdx.x / NJ, j = (int)threadIdx.x % NJ;  // stage-0 lane coordinates
     const int items = (total_rows + RB - 1) / RB;
 
-    float4 h[R0], hn[R0];
-    float4 wv[READW ? R0 : 1], wvn[READW ? R0 : 1];
-    auto load = [&](int item, float4 (&hh)[R0], float4 (&ww)[READW ? R0 : 1]) {
+    float4 h[R0], hn[PF ? R0 : 1];
+    auto load = [&](int item, float4* hh) {
         const int rows = min(RB, total_rows - item * RB);
         const Win w = make_win(v.h0 + (size_t)item * RB * N, (unsigned)(rows * N * 16));
 #pragma unroll
         for (int r = 0; r < R0; ++r) hh[r] = bload4(w, (rr * N + j) * 16, r * NJ * 16);  // past-end rows read 0
-        if constexpr (READW) {
-            const Win w2 = make_win(v.waves + (size_t)item * RB * N, (unsigned)(rows * N * 16));
-#pragma unroll
-            for (int r = 0; r < R0; ++r) ww[r] = bload4(w2, (rr * N + j) * 16, r * NJ * 16);
-        }
     };
-    // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs, so
-    // blockIdx b runs on XCD b % 8.  Give each XCD a contiguous run of rows:
-    // rows y and y+1 share every 128-B line of the tile-major intermediate
-    // (64 B each), and the XCD's L2 then merges the halves into whole-line
-    // write-backs instead of two partial writes from two L2s.
-    const int g = (int)gridDim.x;
-    const int slot = (xcd_remap && g % 8 == 0) ? ((int)blockIdx.x % 8) * (g / 8) + (int)blockIdx.x / 8
-                                                 : (int)blockIdx.x;
-    int item = slot;
-    if (item < items) load(item, h, wv);
-    // DEF: the previous item's outputs are stored during this item's evolve
-    // (4 per texel) instead of in one burst after the last stage.
-    constexpr bool kDef = DEF && (kElems / E::RL == 1) && (NSL % W == 0);
-    float2 pend[kDef ? kElems : 1];
-    float2* pdst = nullptr;  // lane's first output texel of the pending item (null: none / past end)
-    bool have_pend = false;
-    auto store_pend = [&](int q) { pdst[(size_t)q * (NSL / W) * N * W] = pend[q]; };
-    __syncthreads();  // twiddles
-    for (; item < items; item += g) {
-        const int next = item + g;
+    int item = blockIdx.x;
+    if (item < items) load(item, h);
+    __syncthreads();  // twiddles, band
+    for (; item < items; item += gridDim.x) {
+        const int next = item + gridDim.x;
         if constexpr (PF) {
-            if (next < items) load(next, hn, wvn);
+            if (next < items) load(next, hn);
         }
         // stage-0 inputs: plane m of texel x = j + r*NJ of row (item*RB + rr)
         const int row = item * RB + rr;
         const int u = row / N, y = row % N;
-        const WaveBand wb = band[(v.casc0 + u) % v.C];
+        const WaveBand wb = band[u % v.C];
         float2 in[kElems];
 #pragma unroll
         for (int r = 0; r < R0; ++r) {
-            float4 wd;
-            if constexpr (READW) wd = wv[r];
-            else wd = wave_data(j + r * NJ, y, N, wb, v.gravity);
-            const Planes4 o = evolve_texel(h[r], wd, time);
+            const Planes4 o = evolve_texel(h[r], wave_data(j + r * NJ, y, N, wb, v.gravity), time);
 #pragma unroll
             for (int m = 0; m < P; ++m) in[m * R0 + r] = o.p[m];
-            if constexpr (kDef) {
-                if (have_pend && pdst) {
-#pragma unroll
-                    for (int q = r * (kElems / R0); q < (r + 1) * (kElems / R0); ++q) store_pend(q);
-                }
-            }
         }
         // outputs: sequence b = p*RB + rr', element x -> tplane[p][u'][x/W][y'][x%W]
         auto emit = [&](int m, int q, float2 val) {
+            if constexpr (NOSTORE) {
+                asm volatile("" ::"v"(val.x), "v"(val.y));
+                return;
+            }
             int b, jj;
             E::template bj<E::RL>((int)threadIdx.x + m * T, b, jj);
             const int p = b / RB, r2 = b % RB;
             const int row2 = item * RB + r2;
-            if constexpr (SMODE == 2) {  // timing experiment: no stores
-                asm volatile("" ::"v"(val.x), "v"(val.y));
-                return;
-            }
-            if constexpr (kDef) {
-                if (q == 0) {
-                    pdst = nullptr;
-                    if (row2 < total_rows) {
-                        const int u2 = row2 / N, y2 = row2 % N;
-                        pdst = v.tplane + (size_t)p * v.plane_stride + ((size_t)u2 * TILES * N + y2) * W +
-                               (size_t)(jj / W) * N * W + (jj % W);
-                    }
-                }
-                pend[q] = val;
-                return;
-            }
-            if constexpr (SMODE == 1) {  // timing experiment: row-major stores (wrong layout for pass B)
-                if (row2 < total_rows) v.tplane[(size_t)p * v.plane_stride + (size_t)row2 * N + jj + q * NSL] = val;
-                return;
-            }
             if (row2 < total_rows) {
                 const int u2 = row2 / N, y2 = row2 % N;
                 float2* rowp = v.tplane + (size_t)p * v.plane_stride + ((size_t)u2 * TILES * N + y2) * W;
@@ -153,49 +106,21 @@ __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems, WPS) void k_pass_
                 }
             }
         };
-        // PAIR: lane pairs swap so each lane stores 16 B (two consecutive x of one row)
-        auto emit_pair = [&](int m, int q, float4 xy) {
-            int b, jj;
-            E::template bj<E::RL>((int)threadIdx.x + m * T, b, jj);
-            const int p = b / RB, r2 = b % RB;
-            const int row2 = item * RB + r2;
-            if (row2 < total_rows) {
-                const int u2 = row2 / N, y2 = row2 % N;
-                const int x = (jj & ~1) + q * NSL;
-                float2* rowp = v.tplane + (size_t)p * v.plane_stride + ((size_t)u2 * TILES * N + y2) * W;
-                *reinterpret_cast<float4*>(rowp + (size_t)(x / W) * N * W + (x % W)) = xy;
-            }
-        };
-        if constexpr (PAIR) {
-            PairEmit<decltype(emit_pair)> pe{emit_pair};
-            E::run_regs(in, lds, tws, pe);
-        } else {
-            E::run_regs(in, lds, tws, emit);
-        }
-        have_pend = true;
+        E::run_regs(in, lds, tws, emit);
         if constexpr (PF) {
 #pragma unroll
-            for (int r = 0; r < R0; ++r) {
-                h[r] = hn[r];
-                if constexpr (READW) wv[r] = wvn[r];
-            }
+            for (int r = 0; r < R0; ++r) h[r] = hn[r];
         }
         __syncthreads();
         if constexpr (!PF) {
-            if (next < items) load(next, h, wv);
-        }
-    }
-    if constexpr (kDef) {
-        if (have_pend && pdst) {
-#pragma unroll
-            for (int q = 0; q < kElems; ++q) store_pend(q);
+            if (next < items) load(next, h);
         }
     }
 }
 
 // Pass B: one item = (unit, W-column tile); planes in the order DyDxz, DxDz,
-// DxxDzz, DyxDyz with the next plane prefetched into registers.
-template <int N, int P, bool KEEPREG = false, int PFD = 1>
+// DxxDzz, DyxDyz with the next PFD planes prefetched into registers.
+template <int N, int P, int PFD = 1>
 __global__ __launch_bounds__(col_tile(N) * N / kElems) void k_pass_b3(DevView v, int items) {
     using CT = ColTile<N>;
     using E = typename CT::E;
@@ -204,7 +129,7 @@ __global__ __launch_bounds__(col_tile(N) * N / kElems) void k_pass_b3(DevView v,
     constexpr int T = CT::T;
     constexpr int RL = CT::RL;
     constexpr int TILE = W * N;
-    constexpr bool kKeepLds = !KEEPREG && (E::LDS_ELEMS + TW::kLdsEntries + kElems * T) * 8 <= 160 * 1024;
+    constexpr bool kKeepLds = (E::LDS_ELEMS + TW::kLdsEntries + kElems * T) * 8 <= 160 * 1024;
     __shared__ float2 lds[E::LDS_ELEMS];
     __shared__ float2 twl[TW::kLdsEntries];
     __shared__ float2 keep_lds[kKeepLds ? kElems * T : 1];
@@ -321,85 +246,51 @@ int grid3(K kernel, int threads, int items) {
     return items < g ? items : g;
 }
 
-template <int N, int P, int RS = 1, bool READW = false, bool PF = false, int WPS = 0, int SMODE = 0,
-          bool GTW = false, bool PAIR = false, bool CTW = false, bool DEF = false>
+template <int N, int P, int RS, bool PF, bool NOSTORE = false>
 hipError_t go_a3k(const DevView& v, float t, hipStream_t s) {
     constexpr int RB = pa3_rows(N, RS);
     constexpr int T = RB * P * N / kElems;
     const int total = v.units * N;
     const int items = (total + RB - 1) / RB;
-    int g = grid3(k_pass_a3<N, P, RS, READW, PF, WPS, SMODE, GTW, PAIR, CTW, DEF>, T, items);
-    static const int cap = env_int("OCEAN_A3_GRID", 0);
-    if (cap > 0 && g > cap) g = cap;
-    static const int remap = [] {
-        const char* e = std::getenv("OCEAN_XCD_REMAP");
-        return e ? std::atoi(e) : 0;
-    }();
-    hipLaunchKernelGGL((k_pass_a3<N, P, RS, READW, PF, WPS, SMODE, GTW, PAIR, CTW, DEF>), dim3(g), dim3(T), 0, s, v, t,
-                       total, remap);
+    const int g = grid3(k_pass_a3<N, P, RS, PF, NOSTORE>, T, items);
+    hipLaunchKernelGGL((k_pass_a3<N, P, RS, PF, NOSTORE>), dim3(g), dim3(T), 0, s, v, t, total);
     return hipGetLastError();
 }
 
-int a3_variant() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = std::getenv("OCEAN_A3_VARIANT");
-        v = e ? std::atoi(e) : 0;
-    }
-    return v;
-}
-
+// OCEAN_A3_VARIANT selects measured alternatives at N = 1024 (pass A).
 template <int N, int P>
 hipError_t go_a3(const DevView& v, float t, hipStream_t s) {
+    static const int variant = env_int("OCEAN_A3_VARIANT", 0);
     if constexpr (N == 1024 && P == 4) {
-        switch (a3_variant()) {
-            // measured on MI355X, 4 x 1024^2 (profiles/r01_*): RB=1 without prefetch is the default
-            case 1: return go_a3k<N, P, 2, false, true>(v, t, s);   // 2 rows / WG, prefetch: +18 %
-            case 2: return go_a3k<N, P, 2, true, true>(v, t, s);    // + wave data read, not recomputed
-            case 3: return go_a3k<N, P, 1, false, true>(v, t, s);   // prefetch
-            case 4: return go_a3k<N, P, 1, true, false>(v, t, s);   // wave data read
-            case 10: return go_a3k<N, P, 1, false, false, 0, 1>(v, t, s);  // timing only: row-major stores
-            case 11: return go_a3k<N, P, 1, false, false, 0, 2>(v, t, s);  // timing only: no stores
-            case 12: return go_a3k<N, P, 2, false, false, 0, 1>(v, t, s);  // timing only: RB=2 row-major
-            case 5: return go_a3k<N, P, 1, false, false, 0, 0, true>(v, t, s);  // global twiddles (4 WG/CU)
-            case 6: return go_a3k<N, P, 1, false, false, 4, 0, true>(v, t, s);  // + <=128 VGPR
-            case 7: return go_a3k<N, P, 1, false, true, 0, 0, false, true>(v, t, s);  // prefetch + paired 16 B stores
-            case 8: return go_a3k<N, P, 1, false, false, 0, 0, false, true>(v, t, s);  // paired 16 B stores
-            case 9: return go_a3k<N, P, 1, false, true, 0, 0, false, false, true>(v, t, s);  // prefetch + compact tw
-            case 14: return go_a3k<N, P, 1, false, true, 0, 2, false, false, true>(v, t, s);  // timing: 9, no stores
-            case 15: return go_a3k<N, P, 1, false, true, 0, 0, false, false, false, true>(v, t, s);  // PF + deferred stores
-            case 16: return go_a3k<N, P, 1, false, false, 0, 0, false, false, false, true>(v, t, s);  // deferred stores
-            case 17: return go_a3k<N, P, 1, false, true, 0, 0, false, false, true, true>(v, t, s);  // PF+DEF+compact tw
-            case 13: return go_a3k<N, P, 1, false, false, 0, 2, true>(v, t, s);  // timing: no stores, global tw
-            default: break;
+        switch (variant) {
+            case 1: return go_a3k<N, P, 1, false>(v, t, s);       // 1 row / WG, no prefetch
+            case 2: return go_a3k<N, P, 1, true>(v, t, s);        // 1 row / WG, prefetch
+            case 11: return go_a3k<N, P, 2, true, true>(v, t, s);  // timing only: no stores
+            default: return go_a3k<N, P, 2, true>(v, t, s);       // 2 rows / WG (512 lanes), prefetch
         }
     }
-    return go_a3k<N, P>(v, t, s);
+    return go_a3k<N, P, 1, false>(v, t, s);
 }
 
-template <int N, int P, bool KEEPREG, int PFD>
+template <int N, int P, int PFD>
 hipError_t go_b3k(const DevView& v, hipStream_t s) {
     constexpr int W = col_tile(N);
     constexpr int T = W * N / kElems;
     const int items = v.units * (N / W);
-    int g = grid3(k_pass_b3<N, P, KEEPREG, PFD>, T, items);
-    static const int cap = env_int("OCEAN_B3_GRID", 0);
-    if (cap > 0 && g > cap) g = cap;
-    hipLaunchKernelGGL((k_pass_b3<N, P, KEEPREG, PFD>), dim3(g), dim3(T), 0, s, v, items);
+    const int g = grid3(k_pass_b3<N, P, PFD>, T, items);
+    hipLaunchKernelGGL((k_pass_b3<N, P, PFD>), dim3(g), dim3(T), 0, s, v, items);
     return hipGetLastError();
 }
 
+// Two planes in flight at N = 1024 (one workgroup per CU, registers to spare):
+// -3..5 % pass-B time on MI355X; OCEAN_B3_PFD=1 restores one.
 template <int N, int P>
 hipError_t go_b3(const DevView& v, hipStream_t s) {
-    static const int mode = env_int("OCEAN_B3_MODE", 0);
+    static const int pfd = env_int("OCEAN_B3_PFD", 2);
     if constexpr (N == 1024) {
-        switch (mode) {
-            case 1: return go_b3k<N, P, true, 1>(v, s);   // keep values in registers
-            case 2: return go_b3k<N, P, false, 2>(v, s);  // two planes in flight
-            case 3: return go_b3k<N, P, true, 2>(v, s);   // both
-        }
+        if (pfd > 1) return go_b3k<N, P, 2>(v, s);
     }
-    return go_b3k<N, P, false, 1>(v, s);
+    return go_b3k<N, P, 1>(v, s);
 }
 
 }  // namespace

@@ -3,8 +3,6 @@
 // See fft2.hip for the design notes.
 #pragma once
 
-#include <type_traits>
-
 #include "fft_core.h"
 #include "ocean_internal.h"
 
@@ -99,106 +97,6 @@ struct StageTw {
     }
 };
 
-// Compact variant for LDS-tight kernels: a stage with Ns >= 16 keeps only the
-// rows r = 1, 2, 4, 8 of its table (exact, from the double-precision global
-// table) and forms w^r for the other r as products of those (w^3 = w^2 w,
-// w^13 = w^8 w^5, ...: at most three roundings deep, a few ulp).  For the
-// N = 1024, first-radix-4 plan this is 2.5 KiB instead of 8.5 KiB of LDS per
-// workgroup -- the difference between 3 and 4 row workgroups per CU.
-template <int N, int R0>
-struct StageTwCompact {
-    using Full = StageTw<N, R0>;
-    static constexpr int S = n_stages(N, R0);
-    static constexpr bool compact(int s) { return ns_of(N, s, R0) >= 16 && radix_of(N, s, R0) >= 4; }
-    static constexpr int rows(int s) { return compact(s) ? ilog2(radix_of(N, s, R0)) : radix_of(N, s, R0); }
-    static constexpr int off(int s) { return s <= 1 ? 0 : off(s - 1) + ns_of(N, s - 1, R0) * rows(s - 1); }
-    static constexpr int kEntries = off(S) > 0 ? off(S) : 1;
-    static constexpr bool kInLds = true;
-    static constexpr int kLdsEntries = kEntries;
-    static_assert(kEntries * 8 <= 20 * 1024, "compact twiddles must fit LDS");
-    template <int s>
-    static __device__ __forceinline__ void load_stage(float2* lds, const float2* src, int tid, int nthreads) {
-        if constexpr (s < S) {
-            constexpr int NS = ns_of(N, s, R0), RW = rows(s), O = off(s), FO = Full::off(s);
-            constexpr bool CP = compact(s);
-            for (int i = tid; i < NS * RW; i += nthreads) {
-                const int row = i / NS, k = i % NS;
-                const int r = CP ? (1 << row) : row;
-                lds[O + i] = src[FO + r * NS + k];
-            }
-            load_stage<s + 1>(lds, src, tid, nthreads);
-        }
-    }
-    static __device__ __forceinline__ void load(float2* lds, const float2* __restrict__ tw, int tid, int nthreads) {
-        load_stage<1>(lds, Full::global_table(tw), tid, nthreads);
-    }
-    static __device__ __forceinline__ const float2* table(const float2* lds, const float2*) { return lds; }
-    template <int ST>
-    static __device__ __forceinline__ void apply(float2* v, int j, const float2* tws) {
-        constexpr int R = radix_of(N, ST, R0), NS = ns_of(N, ST, R0);
-        if constexpr (NS > 1) {
-            constexpr int O = off(ST);
-            const float2* t = tws + O + (j & (NS - 1));
-            if constexpr (compact(ST)) {
-                float2 w[R];
-#pragma unroll
-                for (int b = 0; (1 << b) < R; ++b) w[1 << b] = t[b * NS];
-#pragma unroll
-                for (int r = 3; r < R; ++r) {
-                    if ((r & (r - 1)) != 0) {
-                        int hb = 1;
-                        while (hb * 2 <= r) hb *= 2;
-                        w[r] = cmul(w[hb], w[r - hb]);
-                    }
-                }
-#pragma unroll
-                for (int r = 1; r < R; ++r) v[r] = cmul(v[r], w[r]);
-            } else {
-#pragma unroll
-                for (int r = 1; r < R; ++r) v[r] = cmul(v[r], t[r * NS]);
-            }
-        }
-    }
-};
-
-// ------------------------------------------------------- block emitters
-// An emitter is either a callable emit(m, q, value) -- one complex output at a
-// time -- or a type with kBlock and block<R>(m, v) that receives a butterfly's
-// R outputs at once (PairEmit below).
-template <class T, class = void>
-struct has_block : std::false_type {};
-template <class T>
-struct has_block<T, std::void_t<decltype(T::kBlock)>> : std::true_type {};
-
-// Lane-pair exchange for 16-byte stores of the last stage: lanes 2i and 2i+1
-// hold elements y and y+1 (consecutive j) at every slot q.  For each slot pair
-// (q0 = 2k, q1 = 2k+1) the even lane ends with elements (y, y+1) of slot q0 and
-// the odd lane with (y, y+1) of slot q1, one DPP swap per pair.  f(m, q, xy,
-// odd) gets the pair; its element index is (j & ~1) + q*Ns.  Requires
-// lane parity == j parity (row-major sequences, Ns even).
-__device__ __forceinline__ float dpp_swap1(float x) {
-    // quad_perm [1,0,3,2]: exchange with the neighbouring lane
-    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, false));
-}
-template <class F>
-struct PairEmit {
-    F& f;
-    static constexpr bool kBlock = true;
-    template <int R>
-    __device__ __forceinline__ void block(int m, const float2* v) const {
-        static_assert(R % 2 == 0, "pair emitter needs an even last radix");
-        const bool odd = (threadIdx.x & 1) != 0;
-#pragma unroll
-        for (int k = 0; k < R; k += 2) {
-            const float2 snd = odd ? v[k] : v[k + 1];
-            const float2 rcv = make_float2(dpp_swap1(snd.x), dpp_swap1(snd.y));
-            const float4 xy = odd ? make_float4(rcv.x, rcv.y, v[k + 1].x, v[k + 1].y)
-                                  : make_float4(v[k].x, v[k].y, rcv.x, rcv.y);
-            f(m, odd ? k + 1 : k, xy);
-        }
-    }
-};
-
 // --------------------------------------------------------------- engine
 // A workgroup transforms B sequences of length N with THREADS = B*N/16
 // lanes, 16 complex values per lane per stage.  Lane -> (sequence b,
@@ -264,12 +162,8 @@ struct Engine {
             TWT::template apply<ST>(&v[m * R], j, tws);
             Idft<R>::run(&v[m * R]);
             if constexpr (LAST) {
-                if constexpr (has_block<Emit>::value) {
-                    emit.template block<R>(m, &v[m * R]);
-                } else {
 #pragma unroll
-                    for (int q = 0; q < R; ++q) emit(m, q, v[m * R + q]);
-                }
+                for (int q = 0; q < R; ++q) emit(m, q, v[m * R + q]);
             } else {
                 const int y0 = (j / NS) * NS * R + (j & (NS - 1));
                 if constexpr (linear()) {

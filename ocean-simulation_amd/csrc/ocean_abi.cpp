@@ -52,11 +52,6 @@ struct ocean_ctx {
     uint32_t flags = 0;
     int variant = 2;  // kernel generation: 1 = fft.hip, 2 = fft2.hip (OCEAN_KERNEL_VARIANT)
     hipStream_t stream = nullptr;
-    // chunked two-stream frame (OCEAN_CHUNKS > 1): pass A of chunk c+1 on `aux`
-    // overlaps pass B of chunk c on `stream`
-    int chunks = 1;
-    hipStream_t aux = nullptr;
-    std::vector<hipEvent_t> chunk_ev;
     // device buffers
     float2* noise = nullptr;
     float4* h0 = nullptr;
@@ -198,8 +193,6 @@ void free_all(ocean_ctx* c) {
         (void)hipEventDestroy(t.b);
     }
     for (auto e : c->event_pool) (void)hipEventDestroy(e);
-    for (hipEvent_t e : c->chunk_ev) (void)hipEventDestroy(e);
-    if (c->aux) (void)hipStreamDestroy(c->aux);
     if (c->stream) (void)hipStreamDestroy(c->stream);
 }
 
@@ -243,7 +236,6 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
     c->P = (flags & OCEAN_F_DISPLACEMENT_ONLY) ? 2 : 4;
     c->noise_set.assign(n_tiles, false);
     if (const char* kv = std::getenv("OCEAN_KERNEL_VARIANT")) c->variant = std::atoi(kv) == 1 ? 1 : 2;
-    if (const char* kc = std::getenv("OCEAN_CHUNKS")) c->chunks = std::max(1, std::atoi(kc));
 
     auto alloc = [&](void** p, size_t bytes) -> bool {
         if (hipMalloc(p, bytes) != hipSuccess) return false;
@@ -424,48 +416,6 @@ int ocean_fill(ocean_ctx* ctx) {
     return timed(ctx, 2, [&] { return ocean::launch_fill(v, ctx->stream); }, "fill");
 }
 
-namespace {
-// View of units [u0, u0 + nu) of a context (fused v3 buffers only).
-ocean::DevView sub_view(const ocean::DevView& v, int u0, int nu) {
-    ocean::DevView s = v;
-    const size_t off = (size_t)u0 * v.n * v.n;
-    s.units = nu;
-    s.casc0 = (v.casc0 + u0) % v.C;
-    s.h0 = v.h0 + off;
-    s.waves = v.waves + off;
-    s.tplane = v.tplane + off;  // plane_stride unchanged: planes stay U * N * N apart
-    if (v.foam) s.foam = v.foam + off;
-    s.disp = v.disp + off;
-    if (v.deriv) s.deriv = v.deriv + off;
-    if (v.turb) s.turb = v.turb + off;
-    if (v.normal) s.normal = v.normal + off;
-    return s;
-}
-
-// Fused frame in K unit chunks over two streams: A(c) on aux, B(c) on the main
-// stream after A(c); A(c+1) runs while B(c) does.  Ordering with the previous
-// frame: aux starts behind everything already queued on the main stream.
-int step_chunked(ocean_ctx* ctx, const ocean::DevView& v, float time) {
-    const int K = ctx->chunks, U = (int)ctx->units(), per = U / K;
-    if (!ctx->aux) OCEAN_HIP(hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
-    while ((int)ctx->chunk_ev.size() < K + 1) {
-        hipEvent_t e = nullptr;
-        OCEAN_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        ctx->chunk_ev.push_back(e);
-    }
-    OCEAN_HIP(hipEventRecord(ctx->chunk_ev[K], ctx->stream));
-    OCEAN_HIP(hipStreamWaitEvent(ctx->aux, ctx->chunk_ev[K], 0));
-    for (int c = 0; c < K; ++c) {
-        const ocean::DevView s = sub_view(v, c * per, per);
-        OCEAN_HIP(ocean::launch_pass_a_v3(s, time, ctx->aux));
-        OCEAN_HIP(hipEventRecord(ctx->chunk_ev[c], ctx->aux));
-        OCEAN_HIP(hipStreamWaitEvent(ctx->stream, ctx->chunk_ev[c], 0));
-        OCEAN_HIP(ocean::launch_pass_b_v3(s, ctx->stream));
-    }
-    return OCEAN_OK;
-}
-}  // namespace
-
 int ocean_step(ocean_ctx* ctx, float time) {
     if (int r = enter(ctx)) return r;
     if (!ctx->spectrum_ready) return fail(OCEAN_E_STATE, "ocean_init_spectrum must precede ocean_step");
@@ -476,8 +426,6 @@ int ocean_step(ocean_ctx* ctx, float time) {
     }
     const ocean::DevView v = ctx->view();
     const bool v3 = ctx->variant == 2 && ocean::pass_v3_supported(ctx->n);
-    const int U = (int)ctx->units();
-    if (v3 && ctx->chunks > 1 && U % ctx->chunks == 0 && !ctx->timing) return step_chunked(ctx, v, time);
     if (int r = timed(ctx, 0, [&] {
             return v3 ? ocean::launch_pass_a_v3(v, time, ctx->stream)
                       : ctx->variant == 2 ? ocean::launch_pass_a_v2(v, time, ctx->stream)

@@ -38,7 +38,6 @@ struct DevView {
     int tile_w;           // column-tile width W = col_tile(N) of the tile-major layouts below
     float2* tplane;       // fused intermediate, P planes x [U][N/W][N][W] (tile-major), stride plane_stride
     float* foam;          // foam state, [U][N/W][N][W] (tile-major); TURB is its broadcast RGBA image
-    int casc0;            // cascade of unit 0 of this view (sub-views over a unit range: u0 % C)
 };
 
 struct SpectrumParams {
