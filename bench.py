@@ -214,6 +214,9 @@ def main():
     ifft_stage = None
     if not args.no_ifft_stage and not cfg["disp_only"]:
         # operator-level stage (IFFT.InverseFastFourierTransform x 4 planes), unfused kernels
+        for _ in range(3):  # first launches load the row/column code objects: keep them out of the timing
+            ctx.ifft2d(0b1111)
+        ctx.synchronize()
         ctx.set_kernel_timing(True)
         ctx.kernel_stats(0), ctx.kernel_stats(1), ctx.kernel_stats(2)
         reps = max(20, args.steps // 5)

@@ -19,6 +19,8 @@
 //    a butterfly are contiguous), copied to LDS when they fit;
 //  * pass B keeps at most two values per texel live across planes
 //    (plane order DyDxz, DxDz, DxxDzz, DyxDyz).
+#include <cstdlib>
+
 #include "fft_engine.h"
 #include "spectrum_math.h"
 
@@ -30,10 +32,9 @@ constexpr int rows_per_item(int N) { return N >= 1024 ? 4 : 4096 / N; }
 
 // Standalone row pass, in place: item = B consecutive rows of the flattened
 // [unit][y] row list of one plane.
-template <int N>
-__global__ __launch_bounds__(rows_per_item(N) * N / kElems) void k_rows2(float2* __restrict__ plane, int total_rows,
-                                                                        const float2* __restrict__ tw) {
-    constexpr int B = rows_per_item(N);
+template <int N, int B = rows_per_item(N)>
+__global__ __launch_bounds__(B * N / kElems) void k_rows2(float2* __restrict__ plane, int total_rows,
+                                                         const float2* __restrict__ tw) {
     using E = Engine<N, B, false, true>;
     using TW = StageTw<N>;
     constexpr int T = E::THREADS;
@@ -318,14 +319,26 @@ hipError_t dispatch_n(int n, A... a) {
 
 template <int N>
 struct Rows2 {
-    static hipError_t go(const DevView* v, int p, int np, hipStream_t s) {
-        constexpr int B = rows_per_item(N);
+    template <int B>
+    static hipError_t go_b(const DevView* v, int p, int np, hipStream_t s) {
         constexpr int T = B * N / kElems;
         const int total = np * v->units * N;
         const int items = (total + B - 1) / B;
-        const int g = persistent_grid(k_rows2<N>, T, items);
-        hipLaunchKernelGGL(k_rows2<N>, dim3(g), dim3(T), 0, s, v->plane[p], total, v->tw);
+        const int g = persistent_grid(k_rows2<N, B>, T, items);
+        hipLaunchKernelGGL((k_rows2<N, B>), dim3(g), dim3(T), 0, s, v->plane[p], total, v->tw);
         return hipGetLastError();
+    }
+    static hipError_t go(const DevView* v, int p, int np, hipStream_t s) {
+        if constexpr (N == 1024) {
+            static const int rb = [] {
+                const char* e = std::getenv("OCEAN_ROWS_B");
+                return e ? std::atoi(e) : 0;
+            }();
+            if (rb == 1) return go_b<1>(v, p, np, s);
+            if (rb == 2) return go_b<2>(v, p, np, s);
+            if (rb == 8) return go_b<8>(v, p, np, s);
+        }
+        return go_b<rows_per_item(N)>(v, p, np, s);
     }
 };
 template <int N>

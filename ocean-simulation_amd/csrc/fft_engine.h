@@ -122,14 +122,34 @@ struct Engine {
         }
     }
     static __device__ __forceinline__ int raw(int b, int y) { return SEQ_FAST ? y * B + b : b * N + y; }
-    static __device__ __forceinline__ int lidx(int b, int y) { return PAD ? pad(raw(b, y)) : raw(b, y); }
+    // Padding.  Rows (b-major): one slot every 16 elements, i + i/16.  Column
+    // tiles (SEQ_FAST, y-major [y][B]): one B-row every 16 rows,
+    // i + (i / 16B) * B -- the radix-16 stage-0 write (rows 16j + q, q < 16)
+    // then spreads the lanes' j over the banks instead of a 16*B*8-byte
+    // stride that maps them all to one bank group.
+    static __device__ __forceinline__ int lidx(int b, int y) {
+        const int i = raw(b, y);
+        return !PAD ? i : (SEQ_FAST ? i + (i / (16 * B)) * B : pad(i));
+    }
     // LDS offset of the k-th element at raw-index stride rs from a butterfly's
-    // base element.  Unpadded: k*rs.  Padded rows (i + i/16): every Stockham
-    // access pattern here has power-of-two strides with the base placed so
-    // that (base % 16) + (k*rs % 16) < 16, hence pad(base + k*rs) =
-    // pad(base) + k*rs + (k*rs)/16 -- a compile-time offset.
-    static constexpr int loff(int k, int rs) { return PAD ? k * rs + (k * rs) / 16 : k * rs; }
-    static constexpr bool linear() { return !PAD || !SEQ_FAST; }
+    // base element, at compile time: pad(base + k*rs) = pad(base) + loff(k, rs).
+    // Rows: every access pattern has power-of-two strides with the base placed
+    // so that (base % 16) + (k*rs % 16) < 16.  Column tiles: the row stride is
+    // a multiple of 16, or 1 from a 16-aligned base (seq_pad_ok()).
+    static constexpr int loff(int k, int rs) {
+        return !PAD ? k * rs : (SEQ_FAST ? k * rs + ((k * rs) / (16 * B)) * B : k * rs + (k * rs) / 16);
+    }
+    static constexpr bool seq_pad_ok() {
+        for (int s = 0; s < S; ++s) {
+            const int R = radix_of(N, s, FIRST), NS = ns_of(N, s, FIRST);
+            if (!((N / R) % 16 == 0 || N / R == 1)) return false;  // reads: rows j + r N/R
+            if (!(NS == 1 || NS % 16 == 0)) return false;           // writes: rows y0 + q NS
+            if (NS == 1 && R > 16) return false;
+        }
+        return true;
+    }
+    static_assert(!(PAD && SEQ_FAST) || seq_pad_ok(), "column-tile padding needs 16-row-aligned strides");
+    static constexpr bool linear() { return true; }
 
     // Stages ST.. from LDS; the last stage hands (m, q, value) to emit.
     template <int ST, class Emit>
@@ -232,7 +252,7 @@ template <int N, int WW = col_tile(N)>
 struct ColTile {
     static constexpr int W = WW;
     static constexpr int tiles = N / W;
-    using E = Engine<N, W, true, false>;
+    using E = Engine<N, W, true, Engine<N, W, true, false>::seq_pad_ok()>;
     static constexpr int T = E::THREADS;
     static constexpr int R0 = E::R0, RL = E::RL;
     static __device__ __forceinline__ int lane_b() { return (int)threadIdx.x % W; }
