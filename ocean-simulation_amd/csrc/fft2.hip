@@ -19,8 +19,6 @@
 //    a butterfly are contiguous), copied to LDS when they fit;
 //  * pass B keeps at most two values per texel live across planes
 //    (plane order DyDxz, DxDz, DxxDzz, DyxDyz).
-#include <cstdlib>
-
 #include "fft_engine.h"
 #include "spectrum_math.h"
 
@@ -329,15 +327,6 @@ struct Rows2 {
         return hipGetLastError();
     }
     static hipError_t go(const DevView* v, int p, int np, hipStream_t s) {
-        if constexpr (N == 1024) {
-            static const int rb = [] {
-                const char* e = std::getenv("OCEAN_ROWS_B");
-                return e ? std::atoi(e) : 0;
-            }();
-            if (rb == 1) return go_b<1>(v, p, np, s);
-            if (rb == 2) return go_b<2>(v, p, np, s);
-            if (rb == 8) return go_b<8>(v, p, np, s);
-        }
         return go_b<rows_per_item(N)>(v, p, np, s);
     }
 };

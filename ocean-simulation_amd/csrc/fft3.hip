@@ -33,7 +33,7 @@ constexpr int pa3_rows(int N, int RS = 2) { return N >= 1024 * RS ? 1 : 1024 * R
 // next item's h0 before this item's transform (its loads are then ahead of
 // this item's stores in the in-order vmcnt queue, so waiting for them never
 // waits for the stores); NOSTORE: timing experiment only (no output).
-template <int N, int P, int RS, bool PF, bool NOSTORE = false>
+template <int N, int P, int RS, bool PF, bool NOSTORE = false, bool NT = false>
 __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems) void k_pass_a3(DevView v, float time, int total_rows) {
     constexpr int RB = pa3_rows(N, RS);
     constexpr int FIRST = 16 / P;
@@ -98,8 +98,9 @@ __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems) void k_pass_a3(De
                 float2* rowp = v.tplane + (size_t)p * v.plane_stride + ((size_t)u2 * TILES * N + y2) * W;
                 if constexpr (NSL % W == 0) {
                     // x = jj + q*NSL: x/W = jj/W + q*NSL/W, x%W = jj%W (compile-time tile stride)
-                    float2* dst = rowp + (size_t)(jj / W) * N * W + (jj % W);
-                    dst[(size_t)q * (NSL / W) * N * W] = val;
+                    float2* dst = rowp + (size_t)(jj / W) * N * W + (jj % W) + (size_t)q * (NSL / W) * N * W;
+                    if constexpr (NT) store2_nt(dst, val);
+                    else *dst = val;
                 } else {
                     const int x = jj + q * NSL;
                     rowp[(size_t)(x / W) * N * W + (x % W)] = val;
@@ -120,7 +121,7 @@ __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems) void k_pass_a3(De
 
 // Pass B: one item = (unit, W-column tile); planes in the order DyDxz, DxDz,
 // DxxDzz, DyxDyz with the next PFD planes prefetched into registers.
-template <int N, int P, int PFD = 1>
+template <int N, int P, int PFD = 1, int NT = 1>
 __global__ __launch_bounds__(col_tile(N) * N / kElems) void k_pass_b3(DevView v, int items) {
     using CT = ColTile<N>;
     using E = typename CT::E;
@@ -156,7 +157,7 @@ __global__ __launch_bounds__(col_tile(N) * N / kElems) void k_pass_b3(DevView v,
     auto load = [&](int item, int p, float2 (&d)[kElems]) {
         const Win w = make_win(v.tplane + (size_t)p * v.plane_stride + (size_t)item * TILE, TILE * 8);
 #pragma unroll
-        for (int i = 0; i < kElems; ++i) d[i] = bload2(w, toff * 8, CT::in_dy(i) * W * 8);
+        for (int i = 0; i < kElems; ++i) d[i] = bload2<(NT & 4) ? 2 : 0>(w, toff * 8, CT::in_dy(i) * W * 8);
     };
 
     // PFD planes in flight ahead of the one being transformed (register ring)
@@ -189,6 +190,16 @@ __global__ __launch_bounds__(col_tile(N) * N / kElems) void k_pass_b3(DevView v,
                     for (int q = 0; q < RL; ++q) fb[m * RL + q] = bload1(rf, toff * 4, CT::out_dy(m, q) * W * 4);
             }
             const Win wd = win16(v.disp, item), wt = win16(v.turb, item), wv = win16(v.deriv, item);
+            // NT bit 0: texture outputs streamed (nontemporal); bit 1: foam state too;
+            // bit 2: intermediate tile loads nontemporal
+            auto st4 = [&](float4 x, const Win& w, int voff, int soff) {
+                if constexpr (NT & 1) gstore4_nt(x, w, voff, soff);
+                else gstore4(x, w, voff, soff);
+            };
+            auto stf = [&](float* a, float x) {
+                if constexpr (NT & 2) store1_nt(a, x);
+                else *a = x;
+            };
             auto emit = [&](int m, int q, float2 val) {
                 const int i = m * RL + q;
                 const int dy = CT::out_dy(m, q);
@@ -198,16 +209,16 @@ __global__ __launch_bounds__(col_tile(N) * N / kElems) void k_pass_b3(DevView v,
                 if (p == 1) {  // DyDxz: keep Dy, Dxz
                     kput(i, make_float2(re, im));
                 } else if (p == 0) {  // DxDz: DISP = (Dx, Dy, Dz, 1)
-                    gstore4(make_float4(re, kget(i).x, im, 1.0f), wd, voff16, so);
+                    st4(make_float4(re, kget(i).x, im, 1.0f), wd, voff16, so);
                 } else if (p == 3) {  // DxxDzz: foam (needs Dxz), then keep Dxx, Dzz
                     const float f = foam_update(fb[i], re, im, kget(i).y);
-                    foam[dy * W] = f;
-                    gstore4(make_float4(f, f, f, f), wt, voff16, so);
+                    stf(&foam[dy * W], f);
+                    st4(make_float4(f, f, f, f), wt, voff16, so);
                     kput(i, make_float2(re, im));
                 } else {  // DyxDyz: DERIV = (Dyx, Dyz, Dxx, Dzz), NORMAL
                     const float2 k = kget(i);
-                    gstore4(make_float4(re, im, k.x, k.y), wv, voff16, so);
-                    if (v.normals) gstore4(normal_from_deriv(re, im, k.x, k.y), win16(v.normal, item), voff16, so);
+                    st4(make_float4(re, im, k.x, k.y), wv, voff16, so);
+                    if (v.normals) st4(normal_from_deriv(re, im, k.x, k.y), win16(v.normal, item), voff16, so);
                 }
             };
             E::run_regs(cur, lds, tws, emit);
@@ -246,14 +257,14 @@ int grid3(K kernel, int threads, int items) {
     return items < g ? items : g;
 }
 
-template <int N, int P, int RS, bool PF, bool NOSTORE = false>
+template <int N, int P, int RS, bool PF, bool NOSTORE = false, bool NT = false>
 hipError_t go_a3k(const DevView& v, float t, hipStream_t s) {
     constexpr int RB = pa3_rows(N, RS);
     constexpr int T = RB * P * N / kElems;
     const int total = v.units * N;
     const int items = (total + RB - 1) / RB;
-    const int g = grid3(k_pass_a3<N, P, RS, PF, NOSTORE>, T, items);
-    hipLaunchKernelGGL((k_pass_a3<N, P, RS, PF, NOSTORE>), dim3(g), dim3(T), 0, s, v, t, total);
+    const int g = grid3(k_pass_a3<N, P, RS, PF, NOSTORE, NT>, T, items);
+    hipLaunchKernelGGL((k_pass_a3<N, P, RS, PF, NOSTORE, NT>), dim3(g), dim3(T), 0, s, v, t, total);
     return hipGetLastError();
 }
 
@@ -266,19 +277,20 @@ hipError_t go_a3(const DevView& v, float t, hipStream_t s) {
             case 1: return go_a3k<N, P, 1, false>(v, t, s);       // 1 row / WG, no prefetch
             case 2: return go_a3k<N, P, 1, true>(v, t, s);        // 1 row / WG, prefetch
             case 11: return go_a3k<N, P, 2, true, true>(v, t, s);  // timing only: no stores
+            case 3: return go_a3k<N, P, 2, true, false, true>(v, t, s);  // nontemporal intermediate stores
             default: return go_a3k<N, P, 2, true>(v, t, s);       // 2 rows / WG (512 lanes), prefetch
         }
     }
     return go_a3k<N, P, 1, false>(v, t, s);
 }
 
-template <int N, int P, int PFD>
+template <int N, int P, int PFD, int NT = 1>
 hipError_t go_b3k(const DevView& v, hipStream_t s) {
     constexpr int W = col_tile(N);
     constexpr int T = W * N / kElems;
     const int items = v.units * (N / W);
-    const int g = grid3(k_pass_b3<N, P, PFD>, T, items);
-    hipLaunchKernelGGL((k_pass_b3<N, P, PFD>), dim3(g), dim3(T), 0, s, v, items);
+    const int g = grid3(k_pass_b3<N, P, PFD, NT>, T, items);
+    hipLaunchKernelGGL((k_pass_b3<N, P, PFD, NT>), dim3(g), dim3(T), 0, s, v, items);
     return hipGetLastError();
 }
 
@@ -287,8 +299,15 @@ hipError_t go_b3k(const DevView& v, hipStream_t s) {
 template <int N, int P>
 hipError_t go_b3(const DevView& v, hipStream_t s) {
     static const int pfd = env_int("OCEAN_B3_PFD", 2);
+    static const int nt = env_int("OCEAN_B3_NT", 1);
     if constexpr (N == 1024) {
-        if (pfd > 1) return go_b3k<N, P, 2>(v, s);
+        if (pfd > 1) {
+            if (nt == 0) return go_b3k<N, P, 2, 0>(v, s);
+            if (nt == 3) return go_b3k<N, P, 2, 3>(v, s);
+            if (nt == 5) return go_b3k<N, P, 2, 5>(v, s);
+            if (nt == 7) return go_b3k<N, P, 2, 7>(v, s);
+            return go_b3k<N, P, 2, 1>(v, s);
+        }
     }
     return go_b3k<N, P, 1>(v, s);
 }

@@ -107,6 +107,61 @@ __global__ void k_wr_a(float2* __restrict__ t, size_t plane_stride, int rows) {
     }
 }
 
+// 6. pass-B memory shape without the FFT: item = (unit, 8-column tile); per
+//    plane a contiguous 64 KiB tile read (next plane prefetched), then for three
+//    planes a float4 texture tile write (8 columns x 1024 rows, 128-B rows) and
+//    the compact foam read + write.  4 units: 369 MB per launch (88 B/texel).
+template <int MODE>  // bit 1: no texture stores, 2: no foam, 4: no tile loads, 8: nontemporal stores
+__global__ __launch_bounds__(512) void k_passb_mem(const float2* __restrict__ tp, size_t ps, float* __restrict__ foam,
+                                                   float4* __restrict__ d0, float4* __restrict__ d1,
+                                                   float4* __restrict__ d2, int items) {
+    constexpr int W = 8, TILE = W * N;
+    const int lb = threadIdx.x % W, lj = threadIdx.x / W;
+    float2 cur[16], nxt[16];
+    auto load = [&](int item, int p, float2* d) {
+        const float2* src = tp + p * ps + (size_t)item * TILE + lj * W + lb;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) d[i] = (MODE & 4) ? make_float2(i + item, p) : src[i * 64 * W];
+    };
+    int item = blockIdx.x;
+    if (item < items) load(item, 0, cur);
+    for (; item < items; item += gridDim.x) {
+        const int u = item / (N / W), x0 = (item % (N / W)) * W;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            if (p < 3) load(item, p + 1, nxt);
+            else if (item + (int)gridDim.x < items) load(item + gridDim.x, 0, nxt);
+            float acc = 0.f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc += cur[i].x - cur[i].y;
+            float4* dst = p == 0 ? d0 : (p == 2 ? d1 : d2);
+            if (p == 3 && !(MODE & 2)) {
+                float* f = foam + (size_t)item * TILE + lj * W + lb;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) f[i * 64 * W] = f[i * 64 * W] * 0.5f + acc;
+            }
+            if (p != 1 && !(MODE & 1)) {
+                float4* o = dst + (size_t)u * N * N + (size_t)lj * N + x0 + lb;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const float4 val = make_float4(acc, cur[i].x, cur[i].y, 1.f);
+                    if (MODE & 8) {
+                        typedef float f4v __attribute__((ext_vector_type(4)));
+                        f4v vv = {val.x, val.y, val.z, val.w};
+                        __builtin_nontemporal_store(vv, reinterpret_cast<f4v*>(&o[(size_t)i * 64 * N]));
+                    } else {
+                        o[(size_t)i * 64 * N] = val;
+                    }
+                }
+            } else if (MODE & 1) {
+                if (acc == 12345.f) d0[threadIdx.x] = make_float4(acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) cur[i] = nxt[i];
+        }
+    }
+}
+
 template <class F>
 float timeit(F f, int reps) {
     hipEvent_t a, b;
@@ -178,6 +233,33 @@ int main() {
                 float ms = timeit(f, reps);
                 printf("%-22s grid %5d %8.1f GB/s  (%.1f us)\n", names[mode], grid, 4.0 * ps * 8 / ms / 1e6, ms * 1e3);
             }
+    }
+    {
+        const int units4 = 4;
+        const size_t ps = (size_t)units4 * N * N;
+        float2* tp;
+        float* fm;
+        float4 *o0, *o1, *o2;
+        CK(hipMalloc(&tp, ps * 8 * 4));
+        CK(hipMalloc(&fm, ps * 4));
+        CK(hipMalloc(&o0, ps * 16));
+        CK(hipMalloc(&o1, ps * 16));
+        CK(hipMalloc(&o2, ps * 16));
+        CK(hipMemset(tp, 0, ps * 32));
+        CK(hipMemset(fm, 0, ps * 4));
+        const int items = units4 * (N / 8);
+        auto run = [&](const char* name, auto kern, double bytes_per_texel) {
+            for (int grid : {256, 512}) {
+                float ms = timeit([&] { hipLaunchKernelGGL(kern, dim3(grid), dim3(512), 0, 0, tp, ps, fm, o0, o1, o2, items); }, reps);
+                printf("passB %-22s grid %4d %8.1f GB/s  (%.1f us)\n", name, grid, bytes_per_texel * ps / ms / 1e6, ms * 1e3);
+            }
+        };
+        run("full shape", k_passb_mem<0>, 88.0);
+        run("no tex stores", k_passb_mem<1>, 40.0);
+        run("no foam", k_passb_mem<2>, 80.0);
+        run("no tile loads", k_passb_mem<4>, 56.0);
+        run("stores only", k_passb_mem<6>, 48.0);
+        run("nt stores", k_passb_mem<8>, 88.0);
     }
     return 0;
 }
