@@ -232,6 +232,150 @@ __global__ __launch_bounds__(col_tile(N) * N / kElems) void k_pass_b3(DevView v,
     }
 }
 
+// Pass A over mirror pairs (N = 1024, P = 4; DESIGN.md "pass A4").  Item i of
+// unit u covers rows y1 = i and y2 = N - i for 0 < i < N/2; item 0 covers rows
+// 0 and N/2, which are their own mirrors and are evolved texel by texel.  The
+// texel k = (x, y1) and its mirror -k = ((N - x) % N, y2) have the same |k|,
+// hence the same wave data up to the signs of kx, kz and the same phase factor
+// exp(i omega t); their h0 halves are each other's conjugates
+// (InitialSpectrum.compute:135-143), so the pair needs h0k at two texels (16 B)
+// instead of h0 at two texels (32 B) and one wave_data + sincos instead of two.
+// Lane j (N/4 lanes) holds stage-0 butterfly j of row y1 and butterfly
+// jm = (NJ - j) % NJ of row y2, whose texels are the mirrors of its own: two
+// radix-4 butterflies x 4 planes = 32 values per lane (Engine EL = 32).
+template <int N, bool NOSTORE = false>
+__global__ __launch_bounds__(N / 4) void k_pass_a4(DevView v, float time, int items_per_unit, int items) {
+    constexpr int P = 4, R0 = 4, RB = 2, EL = 32;
+    using TW = StageTw<N, R0>;
+    using E = Engine<N, RB * P, false, true, R0, TW, EL>;
+    constexpr int T = E::THREADS;
+    constexpr int NJ = N / R0;
+    static_assert(T == NJ && E::R0 == R0, "lane j <-> stage-0 butterfly j");
+    constexpr int W = col_tile(N);
+    constexpr int TILES = N / W;
+    constexpr int NSL = N / E::RL;
+    static_assert(NSL % W == 0, "tile-major emit");
+    __shared__ float2 lds[E::LDS_ELEMS];
+    __shared__ float2 twl[TW::kLdsEntries];
+    TW::load(twl, v.tw, threadIdx.x, T);
+    const float2* tws = TW::table(twl, v.tw);
+    __shared__ WaveBand band[kMaxCascades];
+    if ((int)threadIdx.x < v.C) band[threadIdx.x] = wave_band(v.casc + threadIdx.x * 5);
+    const int j = (int)threadIdx.x;
+    const int jm = (NJ - j) & (NJ - 1);
+    const bool j0 = (j == 0);
+    auto rows_of = [&](int it, int& u, int& y1, int& y2) {
+        u = it / items_per_unit;
+        const int i = it - u * items_per_unit;
+        y1 = i;
+        y2 = i ? N - i : N / 2;
+    };
+    // h0k at texel x_r = j + r NJ of row y1 and at its mirror (N - x_r) % N of row y2
+    auto load_pair = [&](int it, float2 (&a)[R0], float2 (&b)[R0]) {
+        int u, y1, y2;
+        rows_of(it, u, y1, y2);
+        const float2* r1 = v.h0k + ((size_t)u * N + y1) * N;
+        const float2* r2 = v.h0k + ((size_t)u * N + y2) * N;
+#pragma unroll
+        for (int r = 0; r < R0; ++r) {
+            a[r] = r1[j + r * NJ];
+            b[r] = r2[(N - j - r * NJ) & (N - 1)];
+        }
+    };
+    float2 A[R0], B[R0], An[R0], Bn[R0];
+    int item = blockIdx.x;
+    if (item < items) load_pair(item, A, B);
+    __syncthreads();  // twiddles, band
+    for (; item < items; item += gridDim.x) {
+        const int next = item + gridDim.x;
+        if (next < items) load_pair(next, An, Bn);
+        int u, y1, y2;
+        rows_of(item, u, y1, y2);
+        const WaveBand wb = band[u % v.C];
+        float2 in[EL];  // slot (s*4 + p)*4 + r: set s (row y1 / y2), plane p, stage-0 input r
+        if (y1 != 0) {
+            float2 mir[P][R0];  // set-2 values in mirror order (slot r = mirror of set-1 slot r)
+#pragma unroll
+            for (int r = 0; r < R0; ++r) {
+                const int x = j + r * NJ;
+                const float4 wd = wave_data(x, y1, N, wb, v.gravity);
+                const Phase e = evolve_phase(wd.w, time);
+                const Planes4 o = evolve_with(make_float4(A[r].x, A[r].y, B[r].x, -B[r].y), wd, e);
+                // mirror: kx -> -kx (except the Nyquist column x = 0), kz -> -kz, same 1/|k| and omega
+                const float4 wm = make_float4((j0 && r == 0) ? wd.x : -wd.x, wd.y, -wd.z, wd.w);
+                const Planes4 om = evolve_with(make_float4(B[r].x, B[r].y, A[r].x, -A[r].y), wm, e);
+#pragma unroll
+                for (int p = 0; p < P; ++p) {
+                    in[p * R0 + r] = o.p[p];
+                    mir[p][r] = om.p[p];
+                }
+            }
+            // FFT slot r' of butterfly jm holds texel jm + r' NJ = mirror of slot r with
+            // r' = R0 - 1 - r, or (R0 - r) % R0 on lane 0 (jm = 0)
+#pragma unroll
+            for (int p = 0; p < P; ++p)
+#pragma unroll
+                for (int r2 = 0; r2 < R0; ++r2) {
+                    const float2 a = mir[p][R0 - 1 - r2], b = mir[p][(R0 - r2) & (R0 - 1)];
+                    in[(P + p) * R0 + r2] = j0 ? b : a;
+                }
+        } else {
+            // rows 0 and N/2: texels pair inside their row; no sharing (1 item in N/2)
+            float2 am[R0], c[R0];
+            const float2* r1 = v.h0k + ((size_t)u * N + y1) * N;
+            const float2* r2 = v.h0k + ((size_t)u * N + y2) * N;
+#pragma unroll
+            for (int r = 0; r < R0; ++r) {
+                am[r] = r1[(N - j - r * NJ) & (N - 1)];
+                c[r] = r2[j + r * NJ];
+            }
+#pragma unroll
+            for (int r = 0; r < R0; ++r) {
+                const int x = j + r * NJ;
+                const Planes4 o1 = evolve_texel(make_float4(A[r].x, A[r].y, am[r].x, -am[r].y),
+                                                wave_data(x, y1, N, wb, v.gravity), time);
+                const Planes4 o2 = evolve_texel(make_float4(c[r].x, c[r].y, B[r].x, -B[r].y),
+                                                wave_data(x, y2, N, wb, v.gravity), time);
+#pragma unroll
+                for (int p = 0; p < P; ++p) {
+                    in[p * R0 + r] = o1.p[p];
+                    in[(P + p) * R0 + r] = o2.p[p];
+                }
+            }
+        }
+        // stage 0 (radix 4) in registers; sequence b = p * 2 + s
+        const int jb1 = (y1 != 0) ? jm : j;
+#pragma unroll
+        for (int g = 0; g < 2 * P; ++g) {
+            Idft<R0>::run(&in[g * R0]);
+            const int s = g / P, p = g % P;
+            float2* dst = lds + E::lidx(p * RB + s, (s ? jb1 : j) * R0);
+#pragma unroll
+            for (int q = 0; q < R0; ++q) dst[E::loff(q, 1)] = in[g * R0 + q];
+        }
+        __syncthreads();
+        auto emit = [&](int m, int q, float2 val) {
+            if constexpr (NOSTORE) {
+                asm volatile("" ::"v"(val.x), "v"(val.y));
+                return;
+            }
+            int b, jj;
+            E::template bj<E::RL>((int)threadIdx.x + m * T, b, jj);
+            const int p = b / RB, y = (b % RB) ? y2 : y1;
+            float2* dst = v.tplane + (size_t)p * v.plane_stride + ((size_t)u * TILES * N + y) * W +
+                          (size_t)(jj / W) * N * W + (jj % W);
+            dst[(size_t)q * (NSL / W) * N * W] = val;
+        };
+        E::template stages_from<1>(lds, tws, emit);
+#pragma unroll
+        for (int r = 0; r < R0; ++r) {
+            A[r] = An[r];
+            B[r] = Bn[r];
+        }
+        __syncthreads();
+    }
+}
+
 int env_int(const char* name, int dflt) {
     const char* e = std::getenv(name);
     return e ? std::atoi(e) : dflt;
@@ -312,9 +456,27 @@ hipError_t go_b3(const DevView& v, hipStream_t s) {
     return go_b3k<N, P, 1>(v, s);
 }
 
+template <int N, bool NOSTORE = false>
+hipError_t go_a4(const DevView& v, float t, hipStream_t s) {
+    constexpr int T = N / 4;
+    const int ipu = N / 2;
+    const int items = v.units * ipu;
+    const int g = grid3(k_pass_a4<N, NOSTORE>, T, items);
+    hipLaunchKernelGGL((k_pass_a4<N, NOSTORE>), dim3(g), dim3(T), 0, s, v, t, ipu, items);
+    return hipGetLastError();
+}
+
 }  // namespace
 
 bool pass_v3_supported(int n) { return n >= 16 && n <= 1024; }
+
+bool pass_a4_supported(int n, int planes) { return n == 1024 && planes == 4; }
+
+hipError_t launch_pass_a_v4(const DevView& v, float t, hipStream_t s) {
+    if (!pass_a4_supported(v.n, v.planes) || !v.h0k) return hipErrorInvalidValue;
+    static const int nostore = env_int("OCEAN_A4_NOSTORE", 0);
+    return nostore ? go_a4<1024, true>(v, t, s) : go_a4<1024>(v, t, s);
+}
 
 hipError_t launch_pass_a_v3(const DevView& v, float t, hipStream_t s) {
 #define OCEAN_A3(NN)                                                                 \

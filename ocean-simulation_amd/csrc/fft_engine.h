@@ -114,14 +114,15 @@ struct StageTw {
 };
 
 // --------------------------------------------------------------- engine
-// A workgroup transforms B sequences of length N with THREADS = B*N/16
-// lanes, 16 complex values per lane per stage.  Lane -> (sequence b,
+// A workgroup transforms B sequences of length N with THREADS = B*N/EL
+// lanes, EL (16, or 32: two butterflies) complex values per lane per stage.  Lane -> (sequence b,
 // butterfly j) is b-fastest (SEQ_FAST, column tiles) or j-fastest (rows).
 // Stage-0 input slot m*R0 + r is element y = j_m + r*N/R0 of sequence b_m;
 // last-stage output slot (m, q) is element y = j_m + q*N/RL.
-template <int N, int B, bool SEQ_FAST, bool PAD, int FIRST = 16, class TWT = StageTw<N, FIRST>>
+template <int N, int B, bool SEQ_FAST, bool PAD, int FIRST = 16, class TWT = StageTw<N, FIRST>, int EL = kElems>
 struct Engine {
-    static constexpr int THREADS = B * N / kElems;
+    static constexpr int ELEMS = EL;  // complex values per lane per stage (16, or 32 for two butterflies of 16)
+    static constexpr int THREADS = B * N / EL;
     static constexpr int S = n_stages(N, FIRST);
     static constexpr int R0 = radix_of(N, 0, FIRST);
     static constexpr int RL = radix_of(N, S - 1, FIRST);
@@ -172,11 +173,11 @@ struct Engine {
     static __device__ __forceinline__ void stages_from(float2* lds, const float2* tws, Emit& emit) {
         constexpr int R = radix_of(N, ST, FIRST);
         constexpr int NS = ns_of(N, ST, FIRST);
-        constexpr int BF = kElems / R;
+        constexpr int BF = EL / R;
         constexpr bool LAST = (ST == S - 1);
         constexpr int RD = (SEQ_FAST ? B : 1) * (N / R);  // raw stride between a butterfly's inputs
         constexpr int WR = (SEQ_FAST ? B : 1) * NS;       // raw stride between its outputs
-        float2 v[kElems];
+        float2 v[EL];
 #pragma unroll
         for (int m = 0; m < BF; ++m) {
             int b, j;
@@ -234,8 +235,8 @@ struct Engine {
 
     // Full transform from registers (stage-0 layout); LDS free on entry.
     template <class Emit>
-    static __device__ __forceinline__ void run_regs(float2 (&v)[kElems], float2* lds, const float2* tws, Emit& emit) {
-        constexpr int BF = kElems / R0;
+    static __device__ __forceinline__ void run_regs(float2 (&v)[EL], float2* lds, const float2* tws, Emit& emit) {
+        constexpr int BF = EL / R0;
 #pragma unroll
         for (int m = 0; m < BF; ++m) Idft<R0>::run(&v[m * R0]);
         if constexpr (S == 1) {

@@ -55,6 +55,9 @@ struct ocean_ctx {
     // device buffers
     float2* noise = nullptr;
     float4* h0 = nullptr;
+    float2* h0k = nullptr;   // h0.xy for the mirror-pair row pass (pass_a4_supported sizes)
+    bool h0k_valid = false;  // h0k matches h0 (false after ocean_write(H0): .zw may then be arbitrary)
+    int a4 = 1;              // OCEAN_A4=0 selects the v3 row pass
     float4* waves = nullptr;
     float2* plane[4] = {nullptr, nullptr, nullptr, nullptr};
     float4* disp = nullptr;
@@ -91,6 +94,7 @@ struct ocean_ctx {
         v.normals = (flags & OCEAN_F_NORMALS) != 0;
         v.noise = noise;
         v.h0 = h0;
+        v.h0k = h0k;
         v.waves = waves;
         for (int p = 0; p < 4; ++p) v.plane[p] = plane[p];
         v.plane_stride = texels() * units();
@@ -184,7 +188,7 @@ int slice_ptr(ocean_ctx* ctx, int tex, int tile, int cascade, size_t bytes, char
 }
 
 void free_all(ocean_ctx* c) {
-    void* ptrs[] = {c->noise, c->h0,     c->waves, c->plane[0], c->disp, c->deriv,
+    void* ptrs[] = {c->noise, c->h0, c->h0k, c->waves, c->plane[0], c->disp, c->deriv,
                     c->turb,  c->normal, c->tw,    c->casc,     c->tplane, c->foam};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -236,6 +240,7 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
     c->P = (flags & OCEAN_F_DISPLACEMENT_ONLY) ? 2 : 4;
     c->noise_set.assign(n_tiles, false);
     if (const char* kv = std::getenv("OCEAN_KERNEL_VARIANT")) c->variant = std::atoi(kv) == 1 ? 1 : 2;
+    if (const char* ka = std::getenv("OCEAN_A4")) c->a4 = std::atoi(ka);
 
     auto alloc = [&](void** p, size_t bytes) -> bool {
         if (hipMalloc(p, bytes) != hipSuccess) return false;
@@ -245,6 +250,7 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
     bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
     ok = ok && alloc((void**)&c->noise, tex * c->T * 8);
     ok = ok && alloc((void**)&c->h0, tex * U * 16);
+    if (ocean::pass_a4_supported(n, c->P)) ok = ok && alloc((void**)&c->h0k, tex * U * 8);
     ok = ok && alloc((void**)&c->waves, tex * U * 16);
     ok = ok && alloc((void**)&c->plane[0], tex * U * 8 * c->P);  // planes contiguous (one descriptor in pass A)
     if (ok)
@@ -368,6 +374,7 @@ int ocean_init_spectrum(ocean_ctx* ctx) {
     if (ctx->turb) OCEAN_HIP(hipMemsetAsync(ctx->turb, 0, ctx->texels() * ctx->units() * 16, ctx->stream));
     if (ctx->foam) OCEAN_HIP(hipMemsetAsync(ctx->foam, 0, ctx->texels() * ctx->units() * 4, ctx->stream));
     ctx->spectrum_ready = true;
+    ctx->h0k_valid = ctx->h0k != nullptr;
     return OCEAN_OK;
 }
 
@@ -427,6 +434,7 @@ int ocean_step(ocean_ctx* ctx, float time) {
     const ocean::DevView v = ctx->view();
     const bool v3 = ctx->variant == 2 && ocean::pass_v3_supported(ctx->n);
     if (int r = timed(ctx, 0, [&] {
+            if (v3 && ctx->a4 && ctx->h0k_valid) return ocean::launch_pass_a_v4(v, time, ctx->stream);
             return v3 ? ocean::launch_pass_a_v3(v, time, ctx->stream)
                       : ctx->variant == 2 ? ocean::launch_pass_a_v2(v, time, ctx->stream)
                                           : ocean::launch_pass_a(v, time, ctx->stream);
@@ -456,6 +464,7 @@ int ocean_write(ocean_ctx* ctx, int texture, int tile, int cascade, const void* 
     OCEAN_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
     OCEAN_HIP(hipStreamSynchronize(ctx->stream));
     if (texture == OCEAN_TEX_NOISE) ctx->noise_set[tile] = true;
+    if (texture == OCEAN_TEX_H0) ctx->h0k_valid = false;  // the v3 row pass reads h0 (.zw included)
     if (texture == OCEAN_TEX_TURB) {  // foam state follows the uploaded TURB.x (resume)
         const ocean::DevView v = ctx->view();
         OCEAN_HIP(ocean::launch_foam_import(v, ctx->stream));

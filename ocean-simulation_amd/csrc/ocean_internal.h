@@ -24,6 +24,7 @@ struct DevView {
     bool normals;
     const float2* noise;  // [T][N][N]
     float4* h0;           // [U][N][N]
+    float2* h0k;          // [U][N][N] h0(k) alone (= h0.xy); the mirror-pair row pass reads h0(k) and h0(-k) here
     float4* waves;        // [U][N][N]
     float2* plane[4];     // [U][N][N] each; one allocation, plane[p] = plane[0] + p * plane_stride
     size_t plane_stride;  // elements between consecutive planes (U * N * N)
@@ -76,5 +77,9 @@ hipError_t launch_pass_b_v2(const DevView& v, hipStream_t s);
 bool pass_v3_supported(int n);
 hipError_t launch_pass_a_v3(const DevView& v, float t, hipStream_t s);
 hipError_t launch_pass_b_v3(const DevView& v, hipStream_t s);
+// Mirror-pair row pass (N = 1024, 4 planes): one item = rows y and N - y; the
+// texels k and -k share wave data and the phase factor and read h0 once (h0k).
+bool pass_a4_supported(int n, int planes);
+hipError_t launch_pass_a_v4(const DevView& v, float t, hipStream_t s);
 
 }  // namespace ocean

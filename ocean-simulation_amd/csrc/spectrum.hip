@@ -94,6 +94,7 @@ __global__ __launch_bounds__(256) void k_init_spectrum(DevView v, Sp p) {
             h = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         }
         v.h0[i] = h;
+        if (v.h0k) v.h0k[i] = make_float2(h.x, h.y);
         v.waves[i] = w;
     }
 }

@@ -64,12 +64,20 @@ __device__ __forceinline__ void sincos_fast(float x, float* s, float* c) {
     *c = ((q + 1) & 2) ? -cc : cc;
 }
 
-// TimeDependentSpectrum.compute:20-47 for one texel-cascade.
-__device__ __forceinline__ Planes4 evolve_texel(float4 h, float4 w, float t) {
-    Planes4 o;
-    float phase = w.w * t;
+// TimeDependentSpectrum.compute:20-47 for one texel-cascade, split in the
+// phase factor e = exp(i omega t) (:25, shared by k and its mirror -k, which
+// have the same |k| and so the same omega) and the per-texel products.
+struct Phase {
     float ex, ey;
-    sincos_fast(phase, &ey, &ex);
+};
+__device__ __forceinline__ Phase evolve_phase(float omega, float t) {
+    Phase e;
+    sincos_fast(omega * t, &e.ey, &e.ex);
+    return e;
+}
+__device__ __forceinline__ Planes4 evolve_with(float4 h, float4 w, Phase e) {
+    Planes4 o;
+    const float ex = e.ex, ey = e.ey;
     // ComplexMult(h0.xy, e) + ComplexMult(h0.zw, conj(e))  (:26)
     float hx = (h.x * ex - h.y * ey) + (h.z * ex - h.w * (-ey));
     float hy = (h.x * ey + h.y * ex) + (h.z * (-ey) + h.w * ex);
@@ -87,6 +95,9 @@ __device__ __forceinline__ Planes4 evolve_texel(float4 h, float4 w, float t) {
     o.p[2] = make_float2(ydx_x - ydz_y, ydx_y + ydz_x);          // :44 DyxDyz
     o.p[3] = make_float2(dxdx_x - dzdz_y, dxdx_y + dzdz_x);      // :45 DxxDzz
     return o;
+}
+__device__ __forceinline__ Planes4 evolve_texel(float4 h, float4 w, float t) {
+    return evolve_with(h, w, evolve_phase(w.w, t));
 }
 
 // ResultTexturesFiller.compute:27-32: Jacobian and the foam accumulator.

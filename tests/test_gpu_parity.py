@@ -330,3 +330,50 @@ def test_kernel_timing_counts_launches():
     ms_b, nb = ctx.kernel_stats(1)
     assert na == 5 and nb == 5 and ms_a > 0 and ms_b > 0
     ctx.close()
+
+
+def _ctx_with_env(env, n, cas, **kw):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return make_ctx(n, cas, **kw)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def test_mirror_pair_row_pass_bit_identical():
+    """Pass A4 (rows y and N - y per item, texel pairs k / -k sharing wave data and
+    phase) against the per-texel v3 row pass: same arithmetic per texel and per
+    butterfly, so every output bit matches (cfg3 shape, 3 frames incl. foam)."""
+    n, cas = 1024, O.SCENE_CASCADES
+    a, _ = _ctx_with_env({"OCEAN_A4": "1"}, n, cas)
+    b, _ = _ctx_with_env({"OCEAN_A4": "0"}, n, cas)
+    for t in (0.0, 0.5, 250.0):
+        a.step(t)
+        b.step(t)
+    for tex in (oh.TEX_DISP, oh.TEX_DERIV, oh.TEX_TURB):
+        np.testing.assert_array_equal(a.read_all(tex), b.read_all(tex))
+    a.close()
+    b.close()
+
+
+def test_uploaded_h0_uses_full_h0():
+    """After ocean_write(H0) the .zw halves need not be the mirrors' conjugates, so
+    the row pass must read h0 itself (pass A4 reads only h0.xy)."""
+    n, cas = 1024, O.SCENE_CASCADES[:1]
+    a, _ = _ctx_with_env({"OCEAN_A4": "1"}, n, cas)
+    b, _ = _ctx_with_env({"OCEAN_A4": "0"}, n, cas)
+    h0 = a.read(oh.TEX_H0)
+    h0[..., 2:] *= 0.5  # break the conjugate symmetry on purpose
+    a.write(oh.TEX_H0, h0)
+    b.write(oh.TEX_H0, h0)
+    a.step(1.0)
+    b.step(1.0)
+    for tex in (oh.TEX_DISP, oh.TEX_DERIV):
+        np.testing.assert_array_equal(a.read_all(tex), b.read_all(tex))
+    a.close()
+    b.close()
