@@ -171,23 +171,25 @@ __global__ __launch_bounds__(col_tile(N) * N / kElems) void k_pass_b3(DevView v,
     for (; item < items; item += gridDim.x) {
         const int x0 = (item % CT::tiles) * W;
         float* foam = v.foam + (size_t)item * TILE + toff;
+        float fb[kElems];
 #pragma unroll
         for (int pi = 0; pi < P; ++pi) {
             const int p = order[pi];
+            // foam state for the DxxDzz plane: loaded one plane ahead and before that
+            // step's tile prefetch, so waiting for it never waits for the prefetch
+            if (pi + 1 < P && order[pi + 1] == 3) {
+                const Win rf = make_win(v.foam + (size_t)item * TILE, TILE * 4);
+#pragma unroll
+                for (int m = 0; m < kElems / RL; ++m)
+#pragma unroll
+                    for (int q = 0; q < RL; ++q) fb[m * RL + q] = bload1(rf, toff * 4, CT::out_dy(m, q) * W * 4);
+            }
             if constexpr (PFD > 1) {
                 if (pi + 2 < P) load(item, order[pi + 2], nx2);
                 else if (item + (int)gridDim.x < items) load(item + gridDim.x, order[pi + 2 - P], nx2);
             } else {
                 if (pi + 1 < P) load(item, order[pi + 1], nxt);
                 else if (item + (int)gridDim.x < items) load(item + gridDim.x, order[0], nxt);
-            }
-            float fb[kElems];
-            if (p == 3) {
-                const Win rf = make_win(v.foam + (size_t)item * TILE, TILE * 4);
-#pragma unroll
-                for (int m = 0; m < kElems / RL; ++m)
-#pragma unroll
-                    for (int q = 0; q < RL; ++q) fb[m * RL + q] = bload1(rf, toff * 4, CT::out_dy(m, q) * W * 4);
             }
             const Win wd = win16(v.disp, item), wt = win16(v.turb, item), wv = win16(v.deriv, item);
             // NT bit 0: texture outputs streamed (nontemporal); bit 1: foam state too;
