@@ -53,20 +53,12 @@ CONFIGS = {
 }
 
 
-def algorithmic_bytes(n, units, disp_only):
-    """Per-launch algorithmic HBM bytes of the fused schedule, N <= 1024 (v3):
-    pass A: read h0 (16 B; wave data is recomputed), write P planes (8 B each);
-    pass B: read P planes (8 B each) [+ foam state 4 B], write DISP 16 B [+ DERIV 16 B + TURB 16 B
-    + foam state 4 B].  N > 1024 (v2 kernels) additionally read the wave data (16 B) in pass A and
-    read TURB (16 B) instead of the compact foam state in pass B."""
-    tex = n * n * units
-    wave = 16 if n > 1024 else 0
-    foam = (16, 0) if n > 1024 else (4, 4)
-    if disp_only:
-        a, b = 16 + wave + 16, 16 + 16
-    else:
-        a, b = 16 + wave + 32, 32 + foam[0] + 48 + foam[1]
-    return {"pass_a": tex * a, "pass_b": tex * b, "frame": tex * (a + b)}
+def algorithmic_bytes(ctx):
+    """Per-step algorithmic HBM bytes of the schedule the context runs, from the library
+    (ocean_step_bytes): N = 1024 full outputs, pass A4: 8 (h0k) + 32
+    (4 planes) and pass B: 32 (planes) + 4 + 4 (foam state) + 48 (DISP, DERIV, TURB) per texel."""
+    a, b = ctx.step_bytes()
+    return {"pass_a": a, "pass_b": b, "frame": a + b}
 
 
 def pmc_traffic(kernel_substr, profiles_dir=os.path.join(ROOT, "profiles")):
@@ -200,7 +192,7 @@ def main():
     elapsed_ev, _ = reduce_timing(elapsed_ev, tiles, world)
 
     units = tiles * C
-    B = algorithmic_bytes(n, units, cfg["disp_only"])
+    B = algorithmic_bytes(ctx)
     a_us = 1e3 * ka_ms / max(ka_n, 1)
     b_us = 1e3 * kb_ms / max(kb_n, 1)
     dom, dom_us = ("pass_b", b_us) if b_us >= a_us else ("pass_a", a_us)

@@ -170,6 +170,14 @@ int ocean_synchronize(ocean_ctx *ctx);
 int ocean_set_kernel_timing(ocean_ctx *ctx, int enable);
 int ocean_kernel_stats(ocean_ctx *ctx, int kind, double *total_ms, long long *launches);
 
+/* Algorithmic HBM bytes one ocean_step moves in the schedule this context runs
+ * (the roofline numerator; no reference counterpart -- measurement only):
+ * fused: *pass_a = pass A (evolve + row IFFT), *pass_b = pass B (column IFFT +
+ * fill); OCEAN_F_UNFUSED: *pass_a = evolve + row launches, *pass_b = column
+ * launches + fill.  Depends on the kernels selected for N, the flags and the
+ * state (e.g. after ocean_write(H0) pass A reads the full h0). */
+int ocean_step_bytes(ocean_ctx *ctx, uint64_t *pass_a, uint64_t *pass_b);
+
 /* Thread-local message describing the last failure on this thread ("" if none). */
 const char *ocean_last_error(void);
 

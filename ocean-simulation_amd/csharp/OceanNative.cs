@@ -86,6 +86,8 @@ namespace OceanHip
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
         public static extern OceanStatus ocean_kernel_stats(IntPtr ctx, int kind, out double totalMs, out long launches);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
+        public static extern OceanStatus ocean_step_bytes(IntPtr ctx, out ulong passA, out ulong passB);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
         static extern IntPtr ocean_last_error();
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
         public static extern int ocean_abi_version();

@@ -510,6 +510,32 @@ int ocean_set_kernel_timing(ocean_ctx* ctx, int enable) {
     return OCEAN_OK;
 }
 
+int ocean_step_bytes(ocean_ctx* ctx, uint64_t* pass_a, uint64_t* pass_b) {
+    if (!ctx || !pass_a || !pass_b) return fail(OCEAN_E_INVALID_ARG, "null argument");
+    const uint64_t tex = (uint64_t)ctx->texels() * ctx->units();
+    const uint64_t P = ctx->P;
+    const bool full = P == 4, normals = (ctx->flags & OCEAN_F_NORMALS) != 0;
+    const uint64_t outs = 16 + (full ? 32 : 0) + (normals ? 16 : 0);  // DISP [+ DERIV + TURB] [+ NORMAL]
+    uint64_t a = 0, b = 0;
+    if (ctx->flags & OCEAN_F_UNFUSED) {
+        // evolve: h0 + waves -> P planes; rows and columns: read + write every plane;
+        // fill: P planes [+ foam state read + write] -> outputs
+        a = tex * (32 + 8 * P + 16 * P);
+        b = tex * (16 * P + 8 * P + (full ? 8 : 0) + outs);
+    } else if (ctx->variant == 2 && ocean::pass_v3_supported(ctx->n)) {
+        const bool a4 = ctx->a4 && ctx->h0k_valid;
+        a = tex * ((a4 ? 8 : 16) + 8 * P);
+        b = tex * (8 * P + (full ? 8 : 0) + outs);  // + foam state read and write
+    } else {
+        // v1/v2 standard-layout passes: pass A also reads the wave data, pass B the TURB image
+        a = tex * (32 + 8 * P);
+        b = tex * (8 * P + (full ? 16 : 0) + outs);
+    }
+    *pass_a = a;
+    *pass_b = b;
+    return OCEAN_OK;
+}
+
 int ocean_kernel_stats(ocean_ctx* ctx, int kind, double* total_ms, long long* launches) {
     if (int r = enter(ctx)) return r;
     if (kind < 0 || kind > 2 || !total_ms || !launches) return fail(OCEAN_E_INVALID_ARG, "bad kind or null output");

@@ -57,7 +57,7 @@ EXPORTED_SYMBOLS = (
     "ocean_create", "ocean_destroy", "ocean_set_params", "ocean_set_noise", "ocean_generate_noise",
     "ocean_init_spectrum", "ocean_step", "ocean_evolve", "ocean_ifft2d", "ocean_fill", "ocean_read",
     "ocean_write", "ocean_get_device_ptr", "ocean_get_stream", "ocean_synchronize",
-    "ocean_set_kernel_timing", "ocean_kernel_stats", "ocean_last_error", "ocean_abi_version",
+    "ocean_set_kernel_timing", "ocean_kernel_stats", "ocean_step_bytes", "ocean_last_error", "ocean_abi_version",
 )
 
 
@@ -109,6 +109,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "ocean_synchronize": ([P], i),
         "ocean_set_kernel_timing": ([P, i], i),
         "ocean_kernel_stats": ([P, i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong)], i),
+        "ocean_step_bytes": ([P, ctypes.POINTER(u64), ctypes.POINTER(u64)], i),
         "ocean_last_error": ([], ctypes.c_char_p),
         "ocean_abi_version": ([], i),
     }
@@ -225,6 +226,12 @@ class OceanContext:
         ms, cnt = ctypes.c_double(), ctypes.c_longlong()
         _check(self.lib.ocean_kernel_stats(self._h, kind, ctypes.byref(ms), ctypes.byref(cnt)), "ocean_kernel_stats")
         return ms.value, cnt.value
+
+    def step_bytes(self):
+        """(pass A, pass B) algorithmic HBM bytes of one step in this context's schedule."""
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(self.lib.ocean_step_bytes(self._h, ctypes.byref(a), ctypes.byref(b)), "ocean_step_bytes")
+        return a.value, b.value
 
 
 # ---------------------------------------------------------------------------

@@ -377,3 +377,16 @@ def test_uploaded_h0_uses_full_h0():
         np.testing.assert_array_equal(a.read_all(tex), b.read_all(tex))
     a.close()
     b.close()
+
+
+def test_step_bytes_follows_schedule():
+    n, cas = 1024, O.SCENE_CASCADES
+    ctx, _ = make_ctx(n, cas)
+    tex = n * n * len(cas)
+    assert ctx.step_bytes() == (40 * tex, 88 * tex)  # pass A4 (h0k) + pass B
+    ctx.write(oh.TEX_H0, ctx.read(oh.TEX_H0))      # uploaded h0: pass A3 reads all of it
+    assert ctx.step_bytes() == (48 * tex, 88 * tex)
+    ctx.close()
+    d, _ = make_ctx(512, cas[:1], flags=oh.F_DISPLACEMENT_ONLY)
+    assert d.step_bytes() == (32 * 512 * 512, 32 * 512 * 512)
+    d.close()
