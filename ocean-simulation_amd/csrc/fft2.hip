@@ -81,7 +81,7 @@ __global__ __launch_bounds__(cols2_w(N) * N / kElems) void k_cols2(float2* __res
                                                                   const float2* __restrict__ tw) {
     using CT = ColTile<N, cols2_w(N)>;
     using E = typename CT::E;
-    using TW = StageTw<N>;
+    using TW = typename CT::TW;
     constexpr int W = CT::W;
     __shared__ float2 lds[E::LDS_ELEMS];
     __shared__ float2 twl[TW::kLdsEntries];
@@ -193,7 +193,7 @@ template <int N, int P>
 __global__ __launch_bounds__(col_tile(N) * N / kElems) void k_pass_b2(DevView v, int items) {
     using CT = ColTile<N>;
     using E = typename CT::E;
-    using TW = StageTw<N>;
+    using TW = typename CT::TW;
     constexpr int W = CT::W;
     constexpr int T = CT::T;
     constexpr int RL = CT::RL;

@@ -37,12 +37,12 @@ template <int N, int P, int RS, bool PF, bool NOSTORE = false, bool NT = false>
 __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems) void k_pass_a3(DevView v, float time, int total_rows) {
     constexpr int RB = pa3_rows(N, RS);
     constexpr int FIRST = 16 / P;
-    using TW = StageTw<N, FIRST>;
-    using E = Engine<N, RB * P, false, true, FIRST>;
+    using TW = StageTwLds<N, FIRST>;
+    using E = Engine<N, RB * P, false, true, FIRST, TW>;
     constexpr int T = E::THREADS;
     constexpr int R0 = E::R0;             // = FIRST (texels per lane)
     constexpr int NJ = N / R0;            // stage-0 butterflies per sequence
-    constexpr int W = col_tile(N);
+    constexpr int W = inter_w(N);
     constexpr int TILES = N / W;
     constexpr int NSL = N / E::RL;        // last-stage Ns
     static_assert(T / NJ == RB, "stage-0 mapping: lane -> (row, j), butterfly m -> plane m");
@@ -64,7 +64,11 @@ __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems) void k_pass_a3(De
 #pragma unroll
         for (int r = 0; r < R0; ++r) hh[r] = bload4(w, (rr * N + j) * 16, r * NJ * 16);  // past-end rows read 0
     };
-    int item = blockIdx.x;
+    // N >= 2048: the 32-byte tile rows (W = 4) of 4 consecutive rows share each
+    // 128-B line of the intermediate; deal consecutive rows to one XCD (blockIdx b
+    // runs on XCD b % 8) so its L2 merges the partial lines before write-back
+    int item = (N >= 2048 && gridDim.x % 8 == 0) ? (int)(blockIdx.x % 8) * (int)(gridDim.x / 8) + (int)blockIdx.x / 8
+                                                  : (int)blockIdx.x;
     if (item < items) load(item, h);
     __syncthreads();  // twiddles, band
     for (; item < items; item += gridDim.x) {
@@ -121,11 +125,11 @@ __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems) void k_pass_a3(De
 
 // Pass B: one item = (unit, W-column tile); planes in the order DyDxz, DxDz,
 // DxxDzz, DyxDyz with the next PFD planes prefetched into registers.
-template <int N, int P, int PFD = 1, int NT = 1>
+template <int N, int P, int PFD = 1, int NT = 1, bool XR = false>
 __global__ __launch_bounds__(col_tile(N) * N / kElems) void k_pass_b3(DevView v, int items) {
     using CT = ColTile<N>;
     using E = typename CT::E;
-    using TW = StageTw<N>;
+    using TW = typename CT::TW;
     constexpr int W = CT::W;
     constexpr int T = CT::T;
     constexpr int RL = CT::RL;
@@ -161,9 +165,13 @@ __global__ __launch_bounds__(col_tile(N) * N / kElems) void k_pass_b3(DevView v,
     };
 
     // PFD planes in flight ahead of the one being transformed (register ring)
-    float2 cur[kElems], nxt[kElems], nx2[PFD > 1 ? kElems : 1];
-    int item = blockIdx.x;
-    if (item < items) {
+    // (PFD = 0: no prefetch, each plane loaded when its step starts -- N = 4096,
+    // where 1024 lanes leave 128 VGPRs)
+    float2 cur[kElems], nxt[PFD > 0 ? kElems : 1], nx2[PFD > 1 ? kElems : 1];
+    // XR: adjacent tiles (which share 128-B output lines when W * 16 B < 128) on one XCD
+    int item = (XR && gridDim.x % 8 == 0) ? (int)(blockIdx.x % 8) * (int)(gridDim.x / 8) + (int)blockIdx.x / 8
+                                           : (int)blockIdx.x;
+    if (item < items && PFD > 0) {
         load(item, order[0], cur);
         if constexpr (PFD > 1) load(item, order[1], nxt);
     }
@@ -184,7 +192,9 @@ __global__ __launch_bounds__(col_tile(N) * N / kElems) void k_pass_b3(DevView v,
 #pragma unroll
                     for (int q = 0; q < RL; ++q) fb[m * RL + q] = bload1(rf, toff * 4, CT::out_dy(m, q) * W * 4);
             }
-            if constexpr (PFD > 1) {
+            if constexpr (PFD == 0) {
+                load(item, p, cur);
+            } else if constexpr (PFD > 1) {
                 if (pi + 2 < P) load(item, order[pi + 2], nx2);
                 else if (item + (int)gridDim.x < items) load(item + gridDim.x, order[pi + 2 - P], nx2);
             } else {
@@ -226,7 +236,7 @@ __global__ __launch_bounds__(col_tile(N) * N / kElems) void k_pass_b3(DevView v,
             E::run_regs(cur, lds, tws, emit);
 #pragma unroll
             for (int i = 0; i < kElems; ++i) {
-                cur[i] = nxt[i];
+                if constexpr (PFD > 0) cur[i] = nxt[i];
                 if constexpr (PFD > 1) nxt[i] = nx2[i];
             }
             __syncthreads();
@@ -427,16 +437,17 @@ hipError_t go_a3(const DevView& v, float t, hipStream_t s) {
             default: return go_a3k<N, P, 2, true>(v, t, s);       // 2 rows / WG (512 lanes), prefetch
         }
     }
+    if (variant == 11) return go_a3k<N, P, 1, false, true>(v, t, s);  // timing only: no stores
     return go_a3k<N, P, 1, false>(v, t, s);
 }
 
-template <int N, int P, int PFD, int NT = 1>
+template <int N, int P, int PFD, int NT = 1, bool XR = false>
 hipError_t go_b3k(const DevView& v, hipStream_t s) {
     constexpr int W = col_tile(N);
     constexpr int T = W * N / kElems;
     const int items = v.units * (N / W);
-    const int g = grid3(k_pass_b3<N, P, PFD, NT>, T, items);
-    hipLaunchKernelGGL((k_pass_b3<N, P, PFD, NT>), dim3(g), dim3(T), 0, s, v, items);
+    const int g = grid3(k_pass_b3<N, P, PFD, NT, XR>, T, items);
+    hipLaunchKernelGGL((k_pass_b3<N, P, PFD, NT, XR>), dim3(g), dim3(T), 0, s, v, items);
     return hipGetLastError();
 }
 
@@ -446,6 +457,13 @@ template <int N, int P>
 hipError_t go_b3(const DevView& v, hipStream_t s) {
     static const int pfd = env_int("OCEAN_B3_PFD", 2);
     static const int nt = env_int("OCEAN_B3_NT", 1);
+    if constexpr (N == 4096) {
+        static const int m4 = env_int("OCEAN_B4K", 0);
+        if (m4 == 1) return go_b3k<N, P, 0, 0, true>(v, s);
+        if (m4 == 2) return go_b3k<N, P, 0, 1, true>(v, s);
+        if (m4 == 3) return go_b3k<N, P, 0, 0, false>(v, s);
+        return go_b3k<N, P, 0>(v, s);
+    }
     if constexpr (N == 1024) {
         if (pfd > 1) {
             if (nt == 0) return go_b3k<N, P, 2, 0>(v, s);
@@ -470,7 +488,10 @@ hipError_t go_a4(const DevView& v, float t, hipStream_t s) {
 
 }  // namespace
 
-bool pass_v3_supported(int n) { return n >= 16 && n <= 1024; }
+bool pass_v3_supported(int n) {
+    static const int big = env_int("OCEAN_V3_BIG", 1);  // 0: N > 1024 on the v2 kernels (A/B)
+    return n >= 16 && n <= (big ? 4096 : 1024);
+}
 
 bool pass_a4_supported(int n, int planes) { return n == 1024 && planes == 4; }
 
@@ -492,6 +513,8 @@ hipError_t launch_pass_a_v3(const DevView& v, float t, hipStream_t s) {
         OCEAN_A3(256)
         OCEAN_A3(512)
         OCEAN_A3(1024)
+        OCEAN_A3(2048)
+        OCEAN_A3(4096)
     }
 #undef OCEAN_A3
     return hipErrorInvalidValue;
@@ -509,6 +532,8 @@ hipError_t launch_pass_b_v3(const DevView& v, hipStream_t s) {
         OCEAN_B3(256)
         OCEAN_B3(512)
         OCEAN_B3(1024)
+        OCEAN_B3(2048)
+        OCEAN_B3(4096)
     }
 #undef OCEAN_B3
     return hipErrorInvalidValue;

@@ -25,6 +25,9 @@ constexpr int padded(int n) { return n + (n >> 4); }
 
 // column-tile width (columns per workgroup) and row count per workgroup
 constexpr int col_tile(int N) { return (8192 / N) < 4 ? 4 : ((8192 / N) > N ? N : 8192 / N); }
+// width of the fused path's tile-major intermediate and foam state: the column
+// tile for N <= 1024; 16 (128-byte rows) for the four-step column passes above
+constexpr int inter_w(int N) { return N >= 2048 ? 16 : col_tile(N); }
 
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }

@@ -3,6 +3,8 @@
 // See fft2.hip for the design notes.
 #pragma once
 
+#include <type_traits>
+
 #include "fft_core.h"
 #include "ocean_internal.h"
 
@@ -63,6 +65,10 @@ __device__ __forceinline__ void store2_nt(float2* p, float2 x) {
     __builtin_nontemporal_store(v, reinterpret_cast<f32x2*>(p));
 }
 __device__ __forceinline__ void store1_nt(float* p, float x) { __builtin_nontemporal_store(x, p); }
+__device__ __forceinline__ void store4_nt(float4* p, float4 x) {
+    const f32x4 v = {x.x, x.y, x.z, x.w};
+    __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+}
 
 // ------------------------------------------------------------- twiddles
 // Per-stage tables, stage s >= 1 (Ns, R): entry r*Ns + k = exp(+2 pi i r k / (Ns R)),
@@ -112,6 +118,73 @@ struct StageTw {
         }
     }
 };
+
+// Compact variant for N >= 2048, where the full tables do not fit beside a
+// whole-row LDS image: a stage with Ns >= 16 keeps only the rows r = 1, 2, 4,
+// 8 of its table (exact, from the double-precision global table) and forms
+// w^r for the other r as products of those (w^3 = w^2 w, w^13 = w^8 w^5, ...:
+// at most three roundings deep, a few ulp).  N = 4096, first radix 4: 18.5 KiB
+// instead of 41 KiB.  Reading the full table from global memory instead puts
+// twiddle loads behind the previous item's stores in the in-order vmcnt queue.
+template <int N, int R0>
+struct StageTwCompact {
+    using Full = StageTw<N, R0>;
+    static constexpr int S = n_stages(N, R0);
+    static constexpr bool compact(int s) { return ns_of(N, s, R0) >= 16 && radix_of(N, s, R0) >= 2; }
+    static constexpr int rows(int s) { return compact(s) ? ilog2(radix_of(N, s, R0)) : radix_of(N, s, R0); }
+    static constexpr int off(int s) { return s <= 1 ? 0 : off(s - 1) + ns_of(N, s - 1, R0) * rows(s - 1); }
+    static constexpr int kEntries = off(S) > 0 ? off(S) : 1;
+    static constexpr bool kInLds = true;
+    static constexpr int kLdsEntries = kEntries;
+    static_assert(kEntries * 8 <= 32 * 1024, "compact twiddles must fit LDS");
+    template <int s>
+    static __device__ __forceinline__ void load_stage(float2* lds, const float2* src, int tid, int nthreads) {
+        if constexpr (s < S) {
+            constexpr int NS = ns_of(N, s, R0), RW = rows(s), O = off(s), FO = Full::off(s);
+            constexpr bool CP = compact(s);
+            for (int i = tid; i < NS * RW; i += nthreads) {
+                const int row = i / NS, k = i % NS;
+                const int r = CP ? (1 << row) : row;
+                lds[O + i] = src[FO + r * NS + k];
+            }
+            load_stage<s + 1>(lds, src, tid, nthreads);
+        }
+    }
+    static __device__ __forceinline__ void load(float2* lds, const float2* __restrict__ tw, int tid, int nthreads) {
+        load_stage<1>(lds, Full::global_table(tw), tid, nthreads);
+    }
+    static __device__ __forceinline__ const float2* table(const float2* lds, const float2*) { return lds; }
+    template <int ST>
+    static __device__ __forceinline__ void apply(float2* v, int j, const float2* tws) {
+        constexpr int R = radix_of(N, ST, R0), NS = ns_of(N, ST, R0);
+        if constexpr (NS > 1) {
+            constexpr int O = off(ST);
+            const float2* t = tws + O + (j & (NS - 1));
+            if constexpr (compact(ST)) {
+                float2 w[R];
+#pragma unroll
+                for (int b = 0; (1 << b) < R; ++b) w[1 << b] = t[b * NS];
+#pragma unroll
+                for (int r = 3; r < R; ++r) {
+                    if ((r & (r - 1)) != 0) {
+                        int hb = 1;
+                        while (hb * 2 <= r) hb *= 2;
+                        w[r] = cmul(w[hb], w[r - hb]);
+                    }
+                }
+#pragma unroll
+                for (int r = 1; r < R; ++r) v[r] = cmul(v[r], w[r]);
+            } else {
+#pragma unroll
+                for (int r = 1; r < R; ++r) v[r] = cmul(v[r], t[r * NS]);
+            }
+        }
+    }
+};
+
+// LDS twiddle tables for plan (N, R0): the full per-stage tables when they fit, else the compact form.
+template <int N, int R0 = 16>
+using StageTwLds = std::conditional_t<StageTw<N, R0>::kInLds, StageTw<N, R0>, StageTwCompact<N, R0>>;
 
 // --------------------------------------------------------------- engine
 // A workgroup transforms B sequences of length N with THREADS = B*N/EL
@@ -269,10 +342,11 @@ template <int N, int WW = col_tile(N)>
 struct ColTile {
     static constexpr int W = WW;
     static constexpr int tiles = N / W;
+    using TW = StageTwLds<N>;
 #ifdef OCEAN_NO_COLPAD  // A/B builds only
-    using E = Engine<N, W, true, false>;
+    using E = Engine<N, W, true, false, 16, TW>;
 #else
-    using E = Engine<N, W, true, Engine<N, W, true, false>::seq_pad_ok()>;
+    using E = Engine<N, W, true, Engine<N, W, true, false>::seq_pad_ok(), 16, TW>;
 #endif
     static constexpr int T = E::THREADS;
     static constexpr int R0 = E::R0, RL = E::RL;

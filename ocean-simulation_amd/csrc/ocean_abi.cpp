@@ -105,7 +105,7 @@ struct ocean_ctx {
         v.tw = tw;
         v.casc = casc;
         v.gravity = params.gravity;
-        v.tile_w = ocean::fftcore::col_tile(n);
+        v.tile_w = ocean::fftcore::inter_w(n);
         v.tplane = tplane;
         v.foam = foam;
         return v;
@@ -441,6 +441,7 @@ int ocean_step(ocean_ctx* ctx, float time) {
         }, "pass_a"))
         return r;
     return timed(ctx, 1, [&] {
+        if (v3 && ocean::pass_c4_supported(ctx->n)) return ocean::launch_pass_c4(v, ctx->stream);
         return v3 ? ocean::launch_pass_b_v3(v, ctx->stream)
                   : ctx->variant == 2 ? ocean::launch_pass_b_v2(v, ctx->stream) : ocean::launch_pass_b(v, ctx->stream);
     }, "pass_b");
@@ -523,9 +524,10 @@ int ocean_step_bytes(ocean_ctx* ctx, uint64_t* pass_a, uint64_t* pass_b) {
         a = tex * (32 + 8 * P + 16 * P);
         b = tex * (16 * P + 8 * P + (full ? 8 : 0) + outs);
     } else if (ctx->variant == 2 && ocean::pass_v3_supported(ctx->n)) {
-        const bool a4 = ctx->a4 && ctx->h0k_valid;
+        const bool a4 = ctx->a4 && ctx->h0k_valid && ocean::pass_a4_supported(ctx->n, ctx->P);
         a = tex * ((a4 ? 8 : 16) + 8 * P);
         b = tex * (8 * P + (full ? 8 : 0) + outs);  // + foam state read and write
+        if (ocean::pass_c4_supported(ctx->n)) b += tex * 16 * P;  // four-step: step 1 reads + writes the planes
     } else {
         // v1/v2 standard-layout passes: pass A also reads the wave data, pass B the TURB image
         a = tex * (32 + 8 * P);

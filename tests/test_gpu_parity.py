@@ -390,3 +390,19 @@ def test_step_bytes_follows_schedule():
     d, _ = make_ctx(512, cas[:1], flags=oh.F_DISPLACEMENT_ONLY)
     assert d.step_bytes() == (32 * 512 * 512, 32 * 512 * 512)
     d.close()
+
+
+@pytest.mark.parametrize("n", [2048, 4096])
+def test_large_n_fused_vs_unfused(n):
+    """cfg5 sizes: the fused tile-major passes against the unfused operator chain
+    (evolve -> row/column IFFT launches -> fill), 2 frames incl. foam."""
+    cas = O.SCENE_CASCADES[:1]
+    a, _ = make_ctx(n, cas)
+    b, _ = make_ctx(n, cas, flags=oh.F_UNFUSED)
+    for t in (0.5, 100.0):
+        a.step(t)
+        b.step(t)
+    for tex in (oh.TEX_DISP, oh.TEX_DERIV, oh.TEX_TURB):
+        assert_channels(a.read_all(tex), b.read_all(tex), tol=1e-5, what=f"N={n} tex {tex}")
+    a.close()
+    b.close()
