@@ -126,8 +126,8 @@ __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems) void k_pass_a3(De
 // Pass B: one item = (unit, W-column tile); planes in the order DyDxz, DxDz,
 // DxxDzz, DyxDyz with the next PFD planes prefetched into registers.
 template <int N, int P, int PFD = 1, int NT = 1, bool XR = false>
-__global__ __launch_bounds__(col_tile(N) * N / kElems) void k_pass_b3(DevView v, int items) {
-    using CT = ColTile<N>;
+__global__ __launch_bounds__(b3_w(N) * N / kElems) void k_pass_b3(DevView v, int items) {
+    using CT = ColTile<N, b3_w(N)>;
     using E = typename CT::E;
     using TW = typename CT::TW;
     constexpr int W = CT::W;
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(N / 4) void k_pass_a4(DevView v, float time, int it
     constexpr int T = E::THREADS;
     constexpr int NJ = N / R0;
     static_assert(T == NJ && E::R0 == R0, "lane j <-> stage-0 butterfly j");
-    constexpr int W = col_tile(N);
+    constexpr int W = inter_w(N);
     constexpr int TILES = N / W;
     constexpr int NSL = N / E::RL;
     static_assert(NSL % W == 0, "tile-major emit");
@@ -443,7 +443,7 @@ hipError_t go_a3(const DevView& v, float t, hipStream_t s) {
 
 template <int N, int P, int PFD, int NT = 1, bool XR = false>
 hipError_t go_b3k(const DevView& v, hipStream_t s) {
-    constexpr int W = col_tile(N);
+    constexpr int W = b3_w(N);
     constexpr int T = W * N / kElems;
     const int items = v.units * (N / W);
     const int g = grid3(k_pass_b3<N, P, PFD, NT, XR>, T, items);

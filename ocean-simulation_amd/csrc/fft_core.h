@@ -28,6 +28,8 @@ constexpr int col_tile(int N) { return (8192 / N) < 4 ? 4 : ((8192 / N) > N ? N 
 // width of the fused path's tile-major intermediate and foam state: the column
 // tile for N <= 1024; 16 (128-byte rows) for the four-step column passes above
 constexpr int inter_w(int N) { return N >= 2048 ? 16 : col_tile(N); }
+// column-tile width of pass B (N <= 1024; the N >= 2048 column passes are four-step)
+constexpr int b3_w(int N) { return N >= 2048 ? col_tile(N) : inter_w(N); }
 
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
