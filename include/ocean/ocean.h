@@ -55,6 +55,8 @@ extern "C" {
 #define OCEAN_F_NORMALS 0x2u           /* also write the per-cascade NORMAL texture (Water.shader:346-348) */
 #define OCEAN_F_UNFUSED 0x4u           /* ocean_step runs the reference-shaped schedule:
                                           evolve -> 4 x ifft2d -> fill (WaterBody.cs:180-190) */
+#define OCEAN_F_MIPS 0x8u              /* allocate mip chains for DERIV and TURB and regenerate them
+                                          in every ocean_step (WaterBody.cs:191-192, :228-229) */
 
 /* texture ids for ocean_read / ocean_write / ocean_get_device_ptr */
 enum ocean_texture {
@@ -177,6 +179,37 @@ int ocean_kernel_stats(ocean_ctx *ctx, int kind, double *total_ms, long long *la
  * launches + fill.  Depends on the kernels selected for N, the flags and the
  * state (e.g. after ocean_write(H0) pass A reads the full h0). */
 int ocean_step_bytes(ocean_ctx *ctx, uint64_t *pass_a, uint64_t *pass_b);
+
+/* Mip chains (OCEAN_F_MIPS), the GenerateMips of WaterBody.cs:191-192.  Level
+ * L >= 1 of a slice is (N >> L)^2 RGBA fp32 texels, [y][x]; texel (x, y) =
+ * ((a + b) + (c + d)) * 0.25 over the 2x2 texels (2x, 2y), (2x+1, 2y),
+ * (2x, 2y+1), (2x+1, 2y+1) of level L-1 (a box filter: Unity's filter is not
+ * specified).  Level 0 is the texture itself.  `texture` is OCEAN_TEX_DERIV or
+ * OCEAN_TEX_TURB; bytes must equal (N >> level)^2 * 16.  Blocking, like ocean_read.
+ * Device layout (ocean_get_mip_ptr): one chain per slice, levels 1..log2 N
+ * concatenated, slice-major; *ptr points at level `level` of slice 0 and
+ * *slice_stride is the distance in bytes between consecutive slices' chains. */
+int ocean_read_mip(ocean_ctx *ctx, int texture, int tile, int cascade, int level, void *dst, size_t bytes);
+int ocean_get_mip_ptr(ocean_ctx *ctx, int texture, int level, void **ptr, size_t *slice_stride);
+
+/* Asynchronous readback, the AsyncGPUReadback.Request(tex, 0, callback) of
+ * WaterBody.cs:288-296: copies one slice (level 0) to `dst` on a copy stream once
+ * the work queued so far on the ctx stream (e.g. the last ocean_step) has finished,
+ * without blocking the caller.  `dst` must stay valid until the request is done;
+ * for a truly asynchronous copy it should come from ocean_host_alloc (pinned).
+ * ocean_readback_status: 1 done, 0 pending, < 0 error (the request's hasError).
+ * ocean_readback_wait blocks until done.  Every request is freed with
+ * ocean_readback_release (after completion; releasing a pending request waits). */
+typedef struct ocean_readback ocean_readback;
+int ocean_read_async(ocean_ctx *ctx, int texture, int tile, int cascade, void *dst, size_t bytes,
+                     ocean_readback **out);
+int ocean_readback_status(ocean_readback *rb);
+int ocean_readback_wait(ocean_readback *rb);
+void ocean_readback_release(ocean_readback *rb);
+
+/* Pinned host memory for ocean_read_async destinations (hipHostMalloc). */
+int ocean_host_alloc(size_t bytes, void **out);
+void ocean_host_free(void *p);
 
 /* Thread-local message describing the last failure on this thread ("" if none). */
 const char *ocean_last_error(void);

@@ -24,6 +24,7 @@ namespace OceanHip
         DisplacementOnly = 0x1,  // 2 planes -> DISP only
         Normals = 0x2,           // also write the per-cascade NORMAL texture
         Unfused = 0x4,           // reference-shaped schedule: evolve -> 4 x IFFT -> fill
+        Mips = 0x8,              // DERIV / TURB mip chains regenerated every step (GenerateMips)
     }
 
     public enum OceanTexture : int
@@ -87,6 +88,22 @@ namespace OceanHip
         public static extern OceanStatus ocean_kernel_stats(IntPtr ctx, int kind, out double totalMs, out long launches);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
         public static extern OceanStatus ocean_step_bytes(IntPtr ctx, out ulong passA, out ulong passB);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
+        public static extern OceanStatus ocean_read_mip(IntPtr ctx, OceanTexture tex, int tile, int cascade, int level, [Out] float[] dst, UIntPtr bytes);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
+        public static extern OceanStatus ocean_get_mip_ptr(IntPtr ctx, OceanTexture tex, int level, out IntPtr ptr, out UIntPtr sliceStride);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
+        public static extern OceanStatus ocean_read_async(IntPtr ctx, OceanTexture tex, int tile, int cascade, IntPtr dst, UIntPtr bytes, out IntPtr request);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int ocean_readback_status(IntPtr request);   // 1 done, 0 pending, < 0 error (hasError)
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
+        public static extern OceanStatus ocean_readback_wait(IntPtr request);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
+        public static extern void ocean_readback_release(IntPtr request);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
+        public static extern OceanStatus ocean_host_alloc(UIntPtr bytes, out IntPtr ptr);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
+        public static extern void ocean_host_free(IntPtr ptr);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
         static extern IntPtr ocean_last_error();
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]

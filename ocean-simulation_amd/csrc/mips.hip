@@ -1,0 +1,101 @@
+// Mip chains of DERIV and TURB (OCEAN_F_MIPS): GenerateMips of WaterBody.cs:191-192
+// on the two mip-mapped texture arrays (WaterBody.cs:228-229).  Box filter,
+// texel = ((a + b) + (c + d)) * 0.25 of the 2x2 texels below (ocean.h).
+//
+// k_mips_block: one workgroup per 32x32 block of level 0 of one slice builds
+//   levels 1..5 of that block through LDS (each level 0 texel read once).
+// k_mips_tail: one workgroup per slice builds the remaining levels from level 5.
+// Bytes per texel-cascade: read DERIV + TURB (32 B), write 1/3 of that.
+#include "ocean_internal.h"
+
+namespace ocean {
+namespace {
+
+constexpr int kBlk = 32;  // level-0 block per workgroup (levels 1..5)
+
+__device__ __forceinline__ float4 box(float4 a, float4 b, float4 c, float4 d) {
+    return make_float4(((a.x + b.x) + (c.x + d.x)) * 0.25f, ((a.y + b.y) + (c.y + d.y)) * 0.25f,
+                       ((a.z + b.z) + (c.z + d.z)) * 0.25f, ((a.w + b.w) + (c.w + d.w)) * 0.25f);
+}
+
+__device__ __forceinline__ size_t mip_off(int n, int level) {  // texels before `level` in a chain
+    size_t o = 0;
+    for (int l = 1; l < level; ++l) o += (size_t)(n >> l) * (n >> l);
+    return o;
+}
+
+// grid: (blocks per slice, slices, 2 textures); 256 lanes
+__global__ __launch_bounds__(256) void k_mips_block(DevView v, int blk, int levels) {
+    const int n = v.n;
+    const int tex = blockIdx.z;
+    const float4* src = (tex == 0 ? v.deriv : v.turb) + (size_t)blockIdx.y * n * n;
+    float4* chain = (tex == 0 ? v.deriv_mips : v.turb_mips) + (size_t)blockIdx.y * v.mip_chain;
+    const int bpr = n / blk;  // blocks per row
+    const int bx = blockIdx.x % bpr, by = blockIdx.x / bpr;
+    __shared__ float4 cur[kBlk / 2 * kBlk / 2];
+    // level 1: lane t -> texel (t % h, t / h) of the h x h level-1 block, h = blk / 2
+    int h = blk / 2;
+    for (int t = threadIdx.x; t < h * h; t += blockDim.x) {
+        const int x = t % h, y = t / h;
+        const int X = bx * blk + 2 * x, Y = by * blk + 2 * y;
+        const float4 r = box(src[(size_t)Y * n + X], src[(size_t)Y * n + X + 1], src[(size_t)(Y + 1) * n + X],
+                             src[(size_t)(Y + 1) * n + X + 1]);
+        const int m = n >> 1;
+        chain[mip_off(n, 1) + (size_t)(by * h + y) * m + bx * h + x] = r;
+        cur[t] = r;
+    }
+    for (int level = 2; level <= levels; ++level) {
+        __syncthreads();
+        const int hp = h;
+        h >>= 1;
+        float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+        const bool act = (int)threadIdx.x < h * h;
+        if (act) {
+            const int x = threadIdx.x % h, y = threadIdx.x / h;
+            r = box(cur[(2 * y) * hp + 2 * x], cur[(2 * y) * hp + 2 * x + 1], cur[(2 * y + 1) * hp + 2 * x],
+                    cur[(2 * y + 1) * hp + 2 * x + 1]);
+            const int m = n >> level;
+            chain[mip_off(n, level) + (size_t)(by * h + y) * m + bx * h + x] = r;
+        }
+        __syncthreads();
+        if (act) cur[threadIdx.x] = r;
+    }
+}
+
+// grid: (slices, 2 textures); levels first..log2 n from level first-1 in the chain
+__global__ __launch_bounds__(256) void k_mips_tail(DevView v, int first) {
+    const int n = v.n;
+    const int tex = blockIdx.y;
+    float4* chain = (tex == 0 ? v.deriv_mips : v.turb_mips) + (size_t)blockIdx.x * v.mip_chain;
+    for (int level = first; (n >> level) >= 1; ++level) {
+        const int m = n >> level, mp = n >> (level - 1);
+        const float4* s = chain + mip_off(n, level - 1);
+        float4* d = chain + mip_off(n, level);
+        for (int t = threadIdx.x; t < m * m; t += blockDim.x) {
+            const int x = t % m, y = t / m;
+            d[t] = box(s[(2 * y) * mp + 2 * x], s[(2 * y) * mp + 2 * x + 1], s[(2 * y + 1) * mp + 2 * x],
+                       s[(2 * y + 1) * mp + 2 * x + 1]);
+        }
+        __syncthreads();
+    }
+}
+
+}  // namespace
+
+hipError_t launch_mips(const DevView& v, hipStream_t s) {
+    if (!v.deriv_mips || !v.turb_mips) return hipErrorInvalidValue;
+    const int n = v.n;
+    const int blk = n < kBlk ? n : kBlk;
+    int levels = 0;
+    while ((1 << levels) < blk) ++levels;  // levels 1..log2(blk) from the block kernel
+    const int bps = (n / blk) * (n / blk);
+    hipLaunchKernelGGL(k_mips_block, dim3(bps, v.units, 2), dim3(256), 0, s, v, blk, levels);
+    if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+    if (blk < n) {
+        hipLaunchKernelGGL(k_mips_tail, dim3(v.units, 2), dim3(256), 0, s, v, levels + 1);
+        return hipGetLastError();
+    }
+    return hipSuccess;
+}
+
+}  // namespace ocean

@@ -68,6 +68,10 @@ struct ocean_ctx {
     float* casc = nullptr;
     float2* tplane = nullptr;  // fused-path intermediate (tile-major), P planes
     float* foam = nullptr;     // foam state (tile-major)
+    float4* deriv_mips = nullptr;  // OCEAN_F_MIPS chains (levels 1..log2 N per slice)
+    float4* turb_mips = nullptr;
+    size_t mip_chain = 0;
+    hipStream_t copy_stream = nullptr;  // ocean_read_async
     // host state
     ocean::SpectrumParams params{};
     bool params_set = false;
@@ -108,6 +112,9 @@ struct ocean_ctx {
         v.tile_w = ocean::fftcore::inter_w(n);
         v.tplane = tplane;
         v.foam = foam;
+        v.deriv_mips = deriv_mips;
+        v.turb_mips = turb_mips;
+        v.mip_chain = mip_chain;
         return v;
     }
 
@@ -189,7 +196,7 @@ int slice_ptr(ocean_ctx* ctx, int tex, int tile, int cascade, size_t bytes, char
 
 void free_all(ocean_ctx* c) {
     void* ptrs[] = {c->noise, c->h0, c->h0k, c->waves, c->plane[0], c->disp, c->deriv,
-                    c->turb,  c->normal, c->tw,    c->casc,     c->tplane, c->foam};
+                    c->turb,  c->normal, c->tw,    c->casc,     c->tplane, c->foam, c->deriv_mips, c->turb_mips};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& t : c->pending) {
@@ -197,6 +204,7 @@ void free_all(ocean_ctx* c) {
         (void)hipEventDestroy(t.b);
     }
     for (auto e : c->event_pool) (void)hipEventDestroy(e);
+    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     if (c->stream) (void)hipStreamDestroy(c->stream);
 }
 
@@ -217,10 +225,12 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
     if (n_cascades < 1 || n_cascades > ocean::kMaxCascades)
         return fail(OCEAN_E_UNSUPPORTED, "n_cascades must be in [1, 5], got " + std::to_string(n_cascades));
     if (n_tiles < 1) return fail(OCEAN_E_INVALID_ARG, "n_tiles must be >= 1");
-    if (flags & ~(OCEAN_F_DISPLACEMENT_ONLY | OCEAN_F_NORMALS | OCEAN_F_UNFUSED))
+    if (flags & ~(OCEAN_F_DISPLACEMENT_ONLY | OCEAN_F_NORMALS | OCEAN_F_UNFUSED | OCEAN_F_MIPS))
         return fail(OCEAN_E_INVALID_ARG, "unknown flag bits");
     if ((flags & OCEAN_F_DISPLACEMENT_ONLY) && (flags & OCEAN_F_NORMALS))
         return fail(OCEAN_E_INVALID_ARG, "NORMALS needs the derivative planes (not DISPLACEMENT_ONLY)");
+    if ((flags & OCEAN_F_DISPLACEMENT_ONLY) && (flags & OCEAN_F_MIPS))
+        return fail(OCEAN_E_INVALID_ARG, "MIPS chains are on DERIV and TURB (not DISPLACEMENT_ONLY)");
     int ndev = 0;
     hipError_t e = hipGetDeviceCount(&ndev);
     if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
@@ -263,6 +273,11 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
     }
     if (ocean::pass_v3_supported(n)) ok = ok && alloc((void**)&c->tplane, tex * U * 8 * c->P);
     if (flags & OCEAN_F_NORMALS) ok = ok && alloc((void**)&c->normal, tex * U * 16);
+    if (flags & OCEAN_F_MIPS) {
+        for (int l = 1; (n >> l) >= 1; ++l) c->mip_chain += (size_t)(n >> l) * (n >> l);
+        ok = ok && alloc((void**)&c->deriv_mips, c->mip_chain * U * 16);
+        ok = ok && alloc((void**)&c->turb_mips, c->mip_chain * U * 16);
+    }
     const size_t tw_entries = (size_t)n + 128 + ocean::stage_twiddle_entries(n);
     ok = ok && alloc((void**)&c->tw, tw_entries * 8);
     ok = ok && alloc((void**)&c->casc, 5 * 4 * 5);
@@ -423,14 +438,32 @@ int ocean_fill(ocean_ctx* ctx) {
     return timed(ctx, 2, [&] { return ocean::launch_fill(v, ctx->stream); }, "fill");
 }
 
+namespace {
+int step_fused(ocean_ctx* ctx, float time);
+
+// GenerateMips (WaterBody.cs:191-192) when the context has mip chains.
+int generate_mips(ocean_ctx* ctx) {
+    if (!(ctx->flags & OCEAN_F_MIPS)) return OCEAN_OK;
+    const ocean::DevView v = ctx->view();
+    return timed(ctx, 2, [&] { return ocean::launch_mips(v, ctx->stream); }, "mips");
+}
+}  // namespace
+
 int ocean_step(ocean_ctx* ctx, float time) {
     if (int r = enter(ctx)) return r;
     if (!ctx->spectrum_ready) return fail(OCEAN_E_STATE, "ocean_init_spectrum must precede ocean_step");
     if (ctx->flags & OCEAN_F_UNFUSED) {
         if (int r = ocean_evolve(ctx, time)) return r;
         if (int r = ocean_ifft2d(ctx, (1 << ctx->P) - 1)) return r;
-        return ocean_fill(ctx);
+        if (int r = ocean_fill(ctx)) return r;
+        return generate_mips(ctx);
     }
+    if (int r = step_fused(ctx, time)) return r;
+    return generate_mips(ctx);
+}
+
+namespace {
+int step_fused(ocean_ctx* ctx, float time) {
     const ocean::DevView v = ctx->view();
     const bool v3 = ctx->variant == 2 && ocean::pass_v3_supported(ctx->n);
     if (int r = timed(ctx, 0, [&] {
@@ -446,6 +479,7 @@ int ocean_step(ocean_ctx* ctx, float time) {
                   : ctx->variant == 2 ? ocean::launch_pass_b_v2(v, ctx->stream) : ocean::launch_pass_b(v, ctx->stream);
     }, "pass_b");
 }
+}  // namespace
 
 int ocean_read(ocean_ctx* ctx, int texture, int tile, int cascade, void* dst, size_t bytes) {
     if (int r = enter(ctx)) return r;
@@ -455,6 +489,129 @@ int ocean_read(ocean_ctx* ctx, int texture, int tile, int cascade, void* dst, si
     OCEAN_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
     OCEAN_HIP(hipStreamSynchronize(ctx->stream));
     return OCEAN_OK;
+}
+
+namespace {
+// Level `level` (>= 1) of slice (tile, cascade) of DERIV / TURB's mip chain.
+int mip_slice_ptr(ocean_ctx* ctx, int texture, int tile, int cascade, int level, char** out, size_t* bytes) {
+    if (!(ctx->flags & OCEAN_F_MIPS)) return fail(OCEAN_E_STATE, "context created without OCEAN_F_MIPS");
+    if (texture != OCEAN_TEX_DERIV && texture != OCEAN_TEX_TURB)
+        return fail(OCEAN_E_INVALID_ARG, "mip chains exist for OCEAN_TEX_DERIV and OCEAN_TEX_TURB only");
+    if (level < 1 || (ctx->n >> level) < 1) return fail(OCEAN_E_INVALID_ARG, "mip level out of range");
+    if (tile < 0 || tile >= ctx->T || cascade < 0 || cascade >= ctx->C)
+        return fail(OCEAN_E_INVALID_ARG, "tile or cascade out of range");
+    size_t off = 0;
+    for (int l = 1; l < level; ++l) off += (size_t)(ctx->n >> l) * (ctx->n >> l);
+    float4* chain = texture == OCEAN_TEX_DERIV ? ctx->deriv_mips : ctx->turb_mips;
+    const size_t slice = (size_t)tile * ctx->C + cascade;
+    *out = reinterpret_cast<char*>(chain + slice * ctx->mip_chain + off);
+    *bytes = (size_t)(ctx->n >> level) * (ctx->n >> level) * 16;
+    return OCEAN_OK;
+}
+}  // namespace
+
+int ocean_read_mip(ocean_ctx* ctx, int texture, int tile, int cascade, int level, void* dst, size_t bytes) {
+    if (level == 0) return ocean_read(ctx, texture, tile, cascade, dst, bytes);
+    if (int r = enter(ctx)) return r;
+    if (!dst) return fail(OCEAN_E_INVALID_ARG, "null destination");
+    char* src = nullptr;
+    size_t want = 0;
+    if (int r = mip_slice_ptr(ctx, texture, tile, cascade, level, &src, &want)) return r;
+    if (bytes != want)
+        return fail(OCEAN_E_INVALID_ARG, "byte count " + std::to_string(bytes) + " != mip slice size " +
+                                             std::to_string(want));
+    OCEAN_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    OCEAN_HIP(hipStreamSynchronize(ctx->stream));
+    return OCEAN_OK;
+}
+
+int ocean_get_mip_ptr(ocean_ctx* ctx, int texture, int level, void** ptr, size_t* slice_stride) {
+    if (!ctx || !ptr || !slice_stride) return fail(OCEAN_E_INVALID_ARG, "null argument");
+    char* p = nullptr;
+    size_t bytes = 0;
+    if (int r = mip_slice_ptr(ctx, texture, 0, 0, level, &p, &bytes)) return r;
+    *ptr = p;
+    *slice_stride = ctx->mip_chain * 16;
+    return OCEAN_OK;
+}
+
+}  // extern "C"
+
+struct ocean_readback {
+    hipEvent_t done = nullptr;
+    int device = 0;
+};
+
+extern "C" {
+
+int ocean_read_async(ocean_ctx* ctx, int texture, int tile, int cascade, void* dst, size_t bytes,
+                     ocean_readback** out) {
+    if (!out) return fail(OCEAN_E_INVALID_ARG, "out is null");
+    *out = nullptr;
+    if (int r = enter(ctx)) return r;
+    if (!dst) return fail(OCEAN_E_INVALID_ARG, "null destination");
+    char* src = nullptr;
+    if (int r = slice_ptr(ctx, texture, tile, cascade, bytes, &src)) return r;
+    if (!ctx->copy_stream) OCEAN_HIP(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+    ocean_readback* rb = new (std::nothrow) ocean_readback();
+    if (!rb) return fail(OCEAN_E_OUT_OF_MEMORY, "host allocation failed");
+    rb->device = ctx->device;
+    // Snapshot semantics, like a readback in Unity's command stream: a device-side
+    // copy into a staging buffer on the ctx stream (ordered after the queued steps
+    // and before later ones, ~16 MiB at HBM speed), then the host copy on the copy
+    // stream, off the ctx stream's critical path.
+    hipEvent_t after = nullptr;
+    void* stage = nullptr;
+    hipError_t e = hipEventCreateWithFlags(&after, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&rb->done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipMallocAsync(&stage, bytes, ctx->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(stage, src, bytes, hipMemcpyDeviceToDevice, ctx->stream);
+    if (e == hipSuccess) e = hipEventRecord(after, ctx->stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(ctx->copy_stream, after, 0);
+    if (e == hipSuccess) e = hipMemcpyAsync(dst, stage, bytes, hipMemcpyDeviceToHost, ctx->copy_stream);
+    if (e == hipSuccess) e = hipFreeAsync(stage, ctx->copy_stream);
+    if (e == hipSuccess) e = hipEventRecord(rb->done, ctx->copy_stream);
+    if (after) (void)hipEventDestroy(after);  // destruction is deferred until the wait has been resolved
+    if (e != hipSuccess) {
+        if (rb->done) (void)hipEventDestroy(rb->done);
+        delete rb;
+        return hip_fail(e, "ocean_read_async");
+    }
+    *out = rb;
+    return OCEAN_OK;
+}
+
+int ocean_readback_status(ocean_readback* rb) {
+    if (!rb) return fail(OCEAN_E_INVALID_ARG, "null readback");
+    const hipError_t e = hipEventQuery(rb->done);
+    if (e == hipSuccess) return 1;
+    if (e == hipErrorNotReady) return 0;
+    return hip_fail(e, "hipEventQuery");
+}
+
+int ocean_readback_wait(ocean_readback* rb) {
+    if (!rb) return fail(OCEAN_E_INVALID_ARG, "null readback");
+    OCEAN_HIP(hipEventSynchronize(rb->done));
+    return OCEAN_OK;
+}
+
+void ocean_readback_release(ocean_readback* rb) {
+    if (!rb) return;
+    (void)hipEventSynchronize(rb->done);
+    (void)hipEventDestroy(rb->done);
+    delete rb;
+}
+
+int ocean_host_alloc(size_t bytes, void** out) {
+    if (!out || bytes == 0) return fail(OCEAN_E_INVALID_ARG, "null out or zero size");
+    *out = nullptr;
+    const hipError_t e = hipHostMalloc(out, bytes, hipHostMallocDefault);
+    if (e != hipSuccess) return hip_fail(e, "hipHostMalloc");
+    return OCEAN_OK;
+}
+
+void ocean_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
 }
 
 int ocean_write(ocean_ctx* ctx, int texture, int tile, int cascade, const void* src, size_t bytes) {

@@ -39,6 +39,9 @@ struct DevView {
     int tile_w;           // width W = inter_w(N) of the tile-major layouts below
     float2* tplane;       // fused intermediate, P planes x [U][N/W][N][W] (tile-major), stride plane_stride
     float* foam;          // foam state, [U][N/W][N][W] (tile-major); TURB is its broadcast RGBA image
+    float4* deriv_mips;   // OCEAN_F_MIPS: per slice, levels 1..log2 N concatenated (mip_chain texels)
+    float4* turb_mips;
+    size_t mip_chain;     // texels per slice chain: sum over L >= 1 of (N >> L)^2
 };
 
 struct SpectrumParams {
@@ -77,6 +80,9 @@ hipError_t launch_pass_b_v2(const DevView& v, hipStream_t s);
 bool pass_v3_supported(int n);
 hipError_t launch_pass_a_v3(const DevView& v, float t, hipStream_t s);
 hipError_t launch_pass_b_v3(const DevView& v, hipStream_t s);
+// mips.hip: box-filter mip chains of DERIV and TURB (OCEAN_F_MIPS)
+hipError_t launch_mips(const DevView& v, hipStream_t s);
+
 // fft4k.hip (N = 2048, 4096): four-step column passes C1 (in place on the
 // 16-wide tile-major intermediate) + C2 (with the pass-B epilogue); replace pass B.
 bool pass_c4_supported(int n);

@@ -45,6 +45,7 @@ E_OUT_OF_MEMORY = -5
 F_DISPLACEMENT_ONLY = 0x1
 F_NORMALS = 0x2
 F_UNFUSED = 0x4
+F_MIPS = 0x8
 
 TEX_NOISE, TEX_H0, TEX_WAVES = 0, 1, 2
 TEX_PLANE0, TEX_PLANE1, TEX_PLANE2, TEX_PLANE3 = 3, 4, 5, 6
@@ -57,7 +58,9 @@ EXPORTED_SYMBOLS = (
     "ocean_create", "ocean_destroy", "ocean_set_params", "ocean_set_noise", "ocean_generate_noise",
     "ocean_init_spectrum", "ocean_step", "ocean_evolve", "ocean_ifft2d", "ocean_fill", "ocean_read",
     "ocean_write", "ocean_get_device_ptr", "ocean_get_stream", "ocean_synchronize",
-    "ocean_set_kernel_timing", "ocean_kernel_stats", "ocean_step_bytes", "ocean_last_error", "ocean_abi_version",
+    "ocean_set_kernel_timing", "ocean_kernel_stats", "ocean_step_bytes", "ocean_read_mip", "ocean_get_mip_ptr",
+    "ocean_read_async", "ocean_readback_status", "ocean_readback_wait", "ocean_readback_release",
+    "ocean_host_alloc", "ocean_host_free", "ocean_last_error", "ocean_abi_version",
 )
 
 
@@ -110,6 +113,14 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "ocean_set_kernel_timing": ([P, i], i),
         "ocean_kernel_stats": ([P, i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong)], i),
         "ocean_step_bytes": ([P, ctypes.POINTER(u64), ctypes.POINTER(u64)], i),
+        "ocean_read_mip": ([P, i, i, i, i, P, sz], i),
+        "ocean_get_mip_ptr": ([P, i, i, ctypes.POINTER(P), ctypes.POINTER(sz)], i),
+        "ocean_read_async": ([P, i, i, i, P, sz, ctypes.POINTER(P)], i),
+        "ocean_readback_status": ([P], i),
+        "ocean_readback_wait": ([P], i),
+        "ocean_readback_release": ([P], None),
+        "ocean_host_alloc": ([sz, ctypes.POINTER(P)], i),
+        "ocean_host_free": ([P], None),
         "ocean_last_error": ([], ctypes.c_char_p),
         "ocean_abi_version": ([], i),
     }
@@ -208,6 +219,25 @@ class OceanContext:
         a = np.ascontiguousarray(data, np.float32)
         _check(self.lib.ocean_write(self._h, tex, tile, cascade, a.ctypes.data, a.nbytes), "ocean_write")
 
+    def read_mip(self, tex: int, level: int, tile: int = 0, cascade: int = 0) -> np.ndarray:
+        """Level `level` of DERIV / TURB's mip chain (OCEAN_F_MIPS); level 0 = read()."""
+        m = self.n >> level
+        out = np.empty((m, m, 4), np.float32)
+        _check(self.lib.ocean_read_mip(self._h, tex, tile, cascade, level, out.ctypes.data, out.nbytes),
+               "ocean_read_mip")
+        return out
+
+    def mip_ptr(self, tex: int, level: int):
+        """(device pointer of level `level` of slice 0, bytes between slices' chains)."""
+        p, st = ctypes.c_void_p(), ctypes.c_size_t()
+        _check(self.lib.ocean_get_mip_ptr(self._h, tex, level, ctypes.byref(p), ctypes.byref(st)), "ocean_get_mip_ptr")
+        return p.value, st.value
+
+    def read_async(self, tex: int, tile: int = 0, cascade: int = 0) -> "Readback":
+        """AsyncGPUReadback.Request (WaterBody.cs:288-296): copy one slice into pinned
+        host memory once the queued steps finish; poll .done() / .wait(), then .data."""
+        return Readback(self, tex, tile, cascade)
+
     def device_ptr(self, tex: int):
         p, b = ctypes.c_void_p(), ctypes.c_size_t()
         _check(self.lib.ocean_get_device_ptr(self._h, tex, ctypes.byref(p), ctypes.byref(b)), "ocean_get_device_ptr")
@@ -232,6 +262,54 @@ class OceanContext:
         a, b = ctypes.c_uint64(), ctypes.c_uint64()
         _check(self.lib.ocean_step_bytes(self._h, ctypes.byref(a), ctypes.byref(b)), "ocean_step_bytes")
         return a.value, b.value
+
+
+class Readback:
+    """One ocean_read_async request into pinned host memory (ocean_host_alloc)."""
+
+    def __init__(self, ctx: "OceanContext", tex: int, tile: int, cascade: int):
+        self.lib = ctx.lib
+        ch = _TEX_CHANNELS[tex]
+        self.shape = (ctx.n, ctx.n, ch)
+        self.nbytes = ctx.n * ctx.n * ch * 4
+        self._buf = ctypes.c_void_p()
+        self._h = ctypes.c_void_p()
+        _check(self.lib.ocean_host_alloc(self.nbytes, ctypes.byref(self._buf)), "ocean_host_alloc")
+        rc = self.lib.ocean_read_async(ctx._h, tex, tile, cascade, self._buf, self.nbytes, ctypes.byref(self._h))
+        if rc != OK:
+            self.lib.ocean_host_free(self._buf)
+            self._buf = ctypes.c_void_p()
+            _check(rc, "ocean_read_async")
+
+    def done(self) -> bool:
+        rc = self.lib.ocean_readback_status(self._h)
+        if rc < 0:
+            _check(rc, "ocean_readback_status")
+        return rc == 1
+
+    def wait(self) -> None:
+        _check(self.lib.ocean_readback_wait(self._h), "ocean_readback_wait")
+
+    @property
+    def data(self) -> np.ndarray:
+        """A copy of the completed readback (waits if still pending)."""
+        self.wait()
+        raw = (ctypes.c_float * (self.nbytes // 4)).from_address(self._buf.value)
+        return np.frombuffer(raw, np.float32).reshape(self.shape).copy()
+
+    def release(self) -> None:
+        if self._h:
+            self.lib.ocean_readback_release(self._h)
+            self._h = ctypes.c_void_p()
+        if self._buf:
+            self.lib.ocean_host_free(self._buf)
+            self._buf = ctypes.c_void_p()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.release()
+        except Exception:
+            pass
 
 
 # ---------------------------------------------------------------------------

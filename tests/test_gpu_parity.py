@@ -406,3 +406,65 @@ def test_large_n_fused_vs_unfused(n):
         assert_channels(a.read_all(tex), b.read_all(tex), tol=1e-5, what=f"N={n} tex {tex}")
     a.close()
     b.close()
+
+
+# ------------------------------------------------------------- mips + readback
+def _box_chain(level0):
+    """Reference box-filter chain in fp32 with the library's operation order."""
+    out, cur = [], level0.astype(np.float32)
+    while cur.shape[0] > 1:
+        a, b = cur[0::2, 0::2], cur[0::2, 1::2]
+        c, d = cur[1::2, 0::2], cur[1::2, 1::2]
+        cur = ((a + b) + (c + d)) * np.float32(0.25)
+        out.append(cur)
+    return out
+
+
+@pytest.mark.parametrize("n,flags", [(16, 0), (64, 0), (1024, 0), (256, oh.F_UNFUSED)])
+def test_mip_chains_box_filter(n, flags):
+    cas = O.SCENE_CASCADES[:2]
+    ctx, _ = make_ctx(n, cas, flags=flags | oh.F_MIPS)
+    for t in (0.25, 0.5):
+        ctx.step(t)
+    for tex in (oh.TEX_DERIV, oh.TEX_TURB):
+        for c in range(len(cas)):
+            chain = _box_chain(ctx.read(tex, 0, c))
+            for level, ref in enumerate(chain, start=1):
+                np.testing.assert_array_equal(ctx.read_mip(tex, level, 0, c), ref, err_msg=f"tex {tex} level {level}")
+    ctx.close()
+
+
+def test_mip_errors():
+    ctx, _ = make_ctx(32, O.SCENE_CASCADES[:1])
+    with pytest.raises(oh.OceanError) as e:
+        ctx.read_mip(oh.TEX_DERIV, 1)
+    assert e.value.code == oh.E_STATE
+    ctx.close()
+    m, _ = make_ctx(32, O.SCENE_CASCADES[:1], flags=oh.F_MIPS)
+    with pytest.raises(oh.OceanError):
+        m.read_mip(oh.TEX_DISP, 1)
+    with pytest.raises(oh.OceanError):
+        m.read_mip(oh.TEX_DERIV, 6)
+    m.close()
+    with pytest.raises(oh.OceanError) as e:
+        oh.OceanContext(32, 1, 1, oh.F_MIPS | oh.F_DISPLACEMENT_ONLY)
+    assert e.value.code == oh.E_INVALID_ARG
+
+
+def test_async_readback_matches_read():
+    n, cas = 256, O.SCENE_CASCADES
+    ctx, _ = make_ctx(n, cas)
+    ctx.step(0.5)
+    reqs = [ctx.read_async(oh.TEX_DISP, 0, c) for c in range(len(cas))]
+    reqs.append(ctx.read_async(oh.TEX_TURB, 0, 1))
+    ctx.step(1.0)  # after the requests: they snapshot the t = 0.5 frame
+    for c in range(len(cas)):
+        got = reqs[c].data
+        assert reqs[c].done()
+        reqs[c].release()
+        ref = make_ctx(n, cas)[0]
+        ref.step(0.5)
+        np.testing.assert_array_equal(got, ref.read(oh.TEX_DISP, 0, c))
+        ref.close()
+    reqs[-1].release()
+    ctx.close()
