@@ -32,7 +32,7 @@ namespace OceanHip
 
         public void Awake()
         {
-            OceanNative.Check(OceanNative.ocean_create(device, texturesSize, cascades.Length, 1, OceanFlags.None, out ctx),
+            OceanNative.Check(OceanNative.ocean_create(device, texturesSize, cascades.Length, 1, OceanFlags.Mips, out ctx),
                               "ocean_create");
             ApplyParams();
             OceanNative.Check(OceanNative.ocean_generate_noise(ctx, seed), "ocean_generate_noise");
@@ -62,13 +62,31 @@ namespace OceanHip
         public void CalculateWavesTexturesAtTime(float time) =>
             OceanNative.Check(OceanNative.ocean_step(ctx, time), "ocean_step");
 
+        // WaterBody.Update (:284-297): step, then request the displacement slice 0
+        // asynchronously (AsyncGPUReadback.Request, :288-296); a completed request
+        // refreshes buoyancyData, as the reference's callback does.
+        IntPtr pending = IntPtr.Zero, pinned = IntPtr.Zero;
+
         public void Update(float time)
         {
             CalculateWavesTexturesAtTime(time);
-            var buf = buoyancyData ?? new float[texturesSize * texturesSize * 4];
-            OceanNative.Check(OceanNative.ocean_read(ctx, OceanTexture.Displacement, 0, 0, buf,
-                                                     (UIntPtr)(buf.Length * sizeof(float))), "ocean_read");
-            buoyancyData = buf;
+            int n = texturesSize * texturesSize * 4;
+            if (pinned == IntPtr.Zero)
+                OceanNative.Check(OceanNative.ocean_host_alloc((UIntPtr)(n * sizeof(float)), out pinned), "ocean_host_alloc");
+            if (pending != IntPtr.Zero)
+            {
+                int st = OceanNative.ocean_readback_status(pending);
+                if (st == 0) return;                       // previous request still in flight
+                if (st == 1)
+                {
+                    buoyancyData ??= new float[n];
+                    System.Runtime.InteropServices.Marshal.Copy(pinned, buoyancyData, 0, n);
+                }
+                OceanNative.ocean_readback_release(pending); // st < 0: request.hasError, data dropped
+                pending = IntPtr.Zero;
+            }
+            OceanNative.Check(OceanNative.ocean_read_async(ctx, OceanTexture.Displacement, 0, 0, pinned,
+                                                           (UIntPtr)(n * sizeof(float)), out pending), "ocean_read_async");
         }
 
         // WaterBody.cs:195-209, including the mapping over [-texturesSize/2, texturesSize/2].
@@ -95,6 +113,10 @@ namespace OceanHip
 
         public void Dispose()
         {
+            if (pending != IntPtr.Zero) OceanNative.ocean_readback_release(pending);
+            pending = IntPtr.Zero;
+            if (pinned != IntPtr.Zero) OceanNative.ocean_host_free(pinned);
+            pinned = IntPtr.Zero;
             if (ctx != IntPtr.Zero) OceanNative.ocean_destroy(ctx);
             ctx = IntPtr.Zero;
         }

@@ -335,8 +335,10 @@ class WaterBody:
 
     Fields and defaults follow WaterBody.cs:10-33.  Awake() allocates and runs
     the initial spectrum (WaterBody.cs:211-256); CalculateWavesTexturesAtTime(t)
-    is the per-frame path (WaterBody.cs:180-193); Update(t) additionally reads
-    back displacement slice 0 for GetWaterHeight (WaterBody.cs:284-297, 195-209).
+    is the per-frame path (WaterBody.cs:180-193, mip chains of DERIV and TURB
+    included when `mips`); Update(t) additionally requests displacement slice 0
+    asynchronously and, once a request completes, refreshes buoyancyData for
+    GetWaterHeight (AsyncGPUReadback, WaterBody.cs:284-297, 195-209).
     `tiles` > 1 batches independent oceans (tile k uses seed + k).
     """
     windSpeed: float = 1.0
@@ -350,12 +352,14 @@ class WaterBody:
     tiles: int = 1
     displacementOnly: bool = False
     normals: bool = False
+    mips: bool = True  # WaterBody.cs:228-229 creates DERIV / TURB with mip chains
     device: int = 0
     noise: Optional[np.ndarray] = None  # explicit noise texture (tile 0), float32[N][N][2]
 
     def __post_init__(self):
         self.ctx: Optional[OceanContext] = None
         self.buoyancyData: Optional[np.ndarray] = None
+        self._readback: Optional[Readback] = None
 
     def params(self) -> dict:
         return dict(wind_speed=self.windSpeed, wind_dir_x=self.windDirection[0], wind_dir_y=self.windDirection[1],
@@ -363,6 +367,8 @@ class WaterBody:
 
     def Awake(self) -> "WaterBody":
         flags = (F_DISPLACEMENT_ONLY if self.displacementOnly else 0) | (F_NORMALS if self.normals else 0)
+        if self.mips and not self.displacementOnly:
+            flags |= F_MIPS
         self.ctx = OceanContext(self.texturesSize, len(self.cascades), self.tiles, flags, self.device)
         self.ctx.set_params(self.params(), [c.as_dict() for c in self.cascades])
         if self.noise is not None:
@@ -384,7 +390,20 @@ class WaterBody:
 
     def Update(self, time: float) -> None:
         self.CalculateWavesTexturesAtTime(time)
-        self.buoyancyData = self.ctx.read(TEX_DISP, 0, 0)  # AsyncGPUReadback of slice 0 (synchronous here)
+        rb = self._readback
+        if rb is not None:
+            if not rb.done():
+                return  # the previous request is still in flight
+            self.buoyancyData = rb.data
+            rb.release()
+        self._readback = self.ctx.read_async(TEX_DISP, 0, 0)
+
+    def WaitForReadback(self) -> None:
+        """Block until the pending readback (if any) has landed in buoyancyData."""
+        if self._readback is not None:
+            self.buoyancyData = self._readback.data
+            self._readback.release()
+            self._readback = None
 
     def GetWaterHeight(self, worldPosition) -> float:
         """WaterBody.cs:195-209, including its quirk of mapping world x,z over
@@ -412,6 +431,9 @@ class WaterBody:
         return self.ctx.read_all(TEX_TURB, tile)
 
     def OnDisable(self) -> None:
+        if self._readback is not None:
+            self._readback.release()
+            self._readback = None
         if self.ctx is not None:
             self.ctx.close()
             self.ctx = None

@@ -281,7 +281,8 @@ def test_foam_state_resume_via_write():
 # ----------------------------------------------------------- host mirror
 def test_water_body_facade_and_get_water_height():
     wb = oh.scene_water_body(n=256, n_cascades=3, seed=42).Awake()
-    wb.Update(1.5)
+    wb.Update(1.5)            # steps and requests slice 0 asynchronously (AsyncGPUReadback)
+    wb.WaitForReadback()
     disp = wb.DisplacementsTextures()
     assert disp.shape == (3, 256, 256, 4)
     # WaterBody.cs:199-208 mapping: world (x, z) in [-N/2, N/2] -> texel
@@ -290,9 +291,12 @@ def test_water_body_facade_and_get_water_height():
         v = min(max((wz + 128) / 256, 0), 1)
         x, y = min(max(int(u * 256), 0), 255), min(max(int(v * 256), 0), 255)
         assert wb.GetWaterHeight((wx, 0.0, wz)) == disp[0, y, x, 1]
+    assert wb.DerivativesTextures().shape == (3, 256, 256, 4) and wb.ctx.read_mip(oh.TEX_DERIV, 8).shape == (1, 1, 4)
     wb.windSpeed = 12.0
     wb.OnValidate()
     wb.Update(1.5)
+    wb.Update(1.6)            # a later frame may still find the request in flight: never blocks
+    wb.WaitForReadback()
     assert not np.array_equal(wb.DisplacementsTextures(), disp)
     wb.OnDisable()
 
