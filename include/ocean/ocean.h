@@ -119,6 +119,15 @@ int ocean_set_noise(ocean_ctx *ctx, int tile, const float *rg);
  * (WaterBody.cs:71-100).  Generated on the host, uploaded.  Blocking. */
 int ocean_generate_noise(ocean_ctx *ctx, uint64_t seed);
 
+/* On-device noise for large tile batches (replaces the CPU
+ * loop of WaterBody.cs:86-100): a counter-based generator, one independent stream
+ * per texel -- a different sequence from ocean_generate_noise.  Texel (x, y) of
+ * tile t: key = mix(seed + t + G) ^ ((y*N + x) * 0xD1B54A32D192ED03), uniform k
+ * (k = 1, 2, ...) = (mix(key + k*G) >> 40) * 2^-24 with G = 0x9E3779B97F4A7C15 and
+ * mix the splitmix64 finaliser; g1 then g2 each from the Marsaglia polar loop
+ * (WaterBody.cs:71-81).  Blocking. */
+int ocean_generate_noise_device(ocean_ctx *ctx, uint64_t seed);
+
 /* Replaces CalculateInitialSpectrumTextures (WaterBody.cs:171-178):
  * InitialSpectrum.compute:99-129 then :135-143 for every tile and cascade.
  * Also zeroes the foam state (TURB).  Async on the ctx stream. */

@@ -63,6 +63,8 @@ namespace OceanHip
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
         public static extern OceanStatus ocean_generate_noise(IntPtr ctx, ulong seed);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
+        public static extern OceanStatus ocean_generate_noise_device(IntPtr ctx, ulong seed);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
         public static extern OceanStatus ocean_init_spectrum(IntPtr ctx);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
         public static extern OceanStatus ocean_step(IntPtr ctx, float time);

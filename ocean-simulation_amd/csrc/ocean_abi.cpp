@@ -366,6 +366,15 @@ int ocean_set_noise(ocean_ctx* ctx, int tile, const float* rg) {
     return OCEAN_OK;
 }
 
+int ocean_generate_noise_device(ocean_ctx* ctx, uint64_t seed) {
+    if (int r = enter(ctx)) return r;
+    const ocean::DevView v = ctx->view();
+    OCEAN_HIP(ocean::launch_noise(v, seed, ctx->stream));
+    OCEAN_HIP(hipStreamSynchronize(ctx->stream));
+    for (int t = 0; t < ctx->T; ++t) ctx->noise_set[t] = true;
+    return OCEAN_OK;
+}
+
 int ocean_generate_noise(ocean_ctx* ctx, uint64_t seed) {
     if (int r = enter(ctx)) return r;
     std::vector<float> host(ctx->texels() * 2);

@@ -54,6 +54,7 @@ hipError_t launch_conjugate(const DevView& v, hipStream_t s);
 hipError_t launch_evolve(const DevView& v, float t, hipStream_t s);
 hipError_t launch_fill(const DevView& v, hipStream_t s);
 hipError_t launch_foam_import(const DevView& v, hipStream_t s);
+hipError_t launch_noise(const DevView& v, uint64_t seed, hipStream_t s);
 
 // fft.hip
 // Standalone operator (IFFT.InverseFastFourierTransform): in-place row pass and

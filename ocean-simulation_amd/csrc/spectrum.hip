@@ -163,12 +163,55 @@ __global__ __launch_bounds__(256) void k_foam_import(DevView v) {
         v.foam[tiled_index(i, v.n, v.tile_w)] = v.turb[i].x;
 }
 
+// Device noise (ocean_generate_noise_device): a counter-based stream per texel so
+// every texel is independent work.  Texel (x, y) of tile t draws its k-th uniform
+// from h_k = mix(key + (k + 1) * 0x9E3779B97F4A7C15), key = mix(seed + t) ^ (y * N + x)
+// * 0xD1B54A32D192ED03 (mix = the splitmix64 finaliser), U = (h_k >> 40) * 2^-24,
+// and each of g1, g2 comes from the reference's Marsaglia polar loop
+// (WaterBody.cs:71-81: v = 2U - 1, reject s >= 1 or s == 0, keep v1 sqrt(-2 ln s / s)).
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void k_noise(float2* __restrict__ noise, int n, int tiles, uint64_t seed) {
+    const size_t plane = (size_t)n * n;
+    const size_t total = plane * tiles;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const uint64_t t = i / plane, texel = i - t * plane;
+        const uint64_t key = mix64(seed + t + 0x9E3779B97F4A7C15ull) ^ (texel * 0xD1B54A32D192ED03ull);
+        uint64_t k = 0;
+        auto uniform = [&]() {
+            ++k;
+            return (float)(mix64(key + k * 0x9E3779B97F4A7C15ull) >> 40) * (1.0f / 16777216.0f);
+        };
+        float g[2];
+        for (int c = 0; c < 2; ++c) {
+            float v1, v2, q;
+            do {
+                v1 = 2.0f * uniform() - 1.0f;
+                v2 = 2.0f * uniform() - 1.0f;
+                q = v1 * v1 + v2 * v2;
+            } while (q >= 1.0f || q == 0.0f);
+            g[c] = v1 * sqrtf(-2.0f * logf(q) / q);
+        }
+        noise[i] = make_float2(g[0], g[1]);
+    }
+}
+
 unsigned grid_for(size_t total) {
     size_t g = (total + 255) / 256;
     return (unsigned)(g < 16384 ? (g == 0 ? 1 : g) : 16384);
 }
 
 }  // namespace
+
+hipError_t launch_noise(const DevView& v, uint64_t seed, hipStream_t s) {
+    const size_t total = (size_t)v.n * v.n * v.T;
+    hipLaunchKernelGGL(k_noise, dim3(grid_for(total)), dim3(256), 0, s, const_cast<float2*>(v.noise), v.n, v.T, seed);
+    return hipGetLastError();
+}
 
 hipError_t launch_init_spectrum(const DevView& v, const SpectrumParams& sp, hipStream_t s) {
     Sp p{sp.wind_speed, sp.gravity, sp.fetch, sp.depth, sp.wind_dir_x, sp.wind_dir_y};

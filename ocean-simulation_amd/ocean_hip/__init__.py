@@ -59,7 +59,7 @@ EXPORTED_SYMBOLS = (
     "ocean_init_spectrum", "ocean_step", "ocean_evolve", "ocean_ifft2d", "ocean_fill", "ocean_read",
     "ocean_write", "ocean_get_device_ptr", "ocean_get_stream", "ocean_synchronize",
     "ocean_set_kernel_timing", "ocean_kernel_stats", "ocean_step_bytes", "ocean_read_mip", "ocean_get_mip_ptr",
-    "ocean_read_async", "ocean_readback_status", "ocean_readback_wait", "ocean_readback_release",
+    "ocean_generate_noise_device", "ocean_read_async", "ocean_readback_status", "ocean_readback_wait", "ocean_readback_release",
     "ocean_host_alloc", "ocean_host_free", "ocean_last_error", "ocean_abi_version",
 )
 
@@ -114,6 +114,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "ocean_kernel_stats": ([P, i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong)], i),
         "ocean_step_bytes": ([P, ctypes.POINTER(u64), ctypes.POINTER(u64)], i),
         "ocean_read_mip": ([P, i, i, i, i, P, sz], i),
+        "ocean_generate_noise_device": ([P, u64], i),
         "ocean_get_mip_ptr": ([P, i, i, ctypes.POINTER(P), ctypes.POINTER(sz)], i),
         "ocean_read_async": ([P, i, i, i, P, sz, ctypes.POINTER(P)], i),
         "ocean_readback_status": ([P], i),
@@ -187,6 +188,10 @@ class OceanContext:
         _check(self.lib.ocean_generate_noise(self._h, ctypes.c_uint64(seed)), "ocean_generate_noise")
 
     # -- compute --------------------------------------------------------------
+    def generate_noise_device(self, seed: int) -> None:
+        """Counter-based noise generated on the GPU for every tile (ocean.h)."""
+        _check(self.lib.ocean_generate_noise_device(self._h, seed), "ocean_generate_noise_device")
+
     def init_spectrum(self) -> None:
         _check(self.lib.ocean_init_spectrum(self._h), "ocean_init_spectrum")
 

@@ -90,6 +90,46 @@ def generate_noise(n: int, seed: int) -> np.ndarray:
     return out
 
 
+_G = np.uint64(0x9E3779B97F4A7C15)
+
+
+def _mix64(z):
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def generate_noise_device(n: int, tiles: int, seed: int) -> np.ndarray:
+    """Restatement of the library's on-device noise (ocean.h ocean_generate_noise_device):
+    per texel a counter-based uniform stream, each of g1, g2 from the polar loop of
+    WaterBody.cs:71-81.  Rejection decisions are exact; g differs from the device only by
+    the ulp-level difference of logf.  float32 [tiles][N][N][2]."""
+    with np.errstate(over="ignore"):
+        texel = np.arange(n * n, dtype=np.uint64)
+        out = np.empty((tiles, n * n, 2), np.float32)
+        for t in range(tiles):
+            key = _mix64(np.uint64(seed) + np.uint64(t) + _G) ^ (texel * np.uint64(0xD1B54A32D192ED03))
+            k = np.zeros(n * n, np.uint64)
+
+            def uniform(idx):
+                k[idx] += np.uint64(1)
+                h = _mix64(key[idx] + k[idx] * _G)
+                return (h >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+            for c in range(2):
+                g = np.empty(n * n, np.float32)
+                todo = np.arange(n * n)
+                while todo.size:
+                    v1 = np.float32(2.0) * uniform(todo) - np.float32(1.0)
+                    v2 = np.float32(2.0) * uniform(todo) - np.float32(1.0)
+                    q = v1 * v1 + v2 * v2
+                    ok = (q < np.float32(1.0)) & (q != np.float32(0.0))
+                    qa = q[ok]
+                    g[todo[ok]] = v1[ok] * np.sqrt(np.float32(-2.0) * np.log(qa) / qa)
+                    todo = todo[~ok]
+                out[t, :, c] = g
+    return out.reshape(tiles, n, n, 2)
+
+
 def init_spectrum(n, params, cascades, noise, conjugate=True):
     C = len(cascades)
     h0 = np.empty((C, n, n, 4), np.float32)

@@ -472,3 +472,19 @@ def test_async_readback_matches_read():
         ref.close()
     reqs[-1].release()
     ctx.close()
+
+
+def test_device_noise_matches_restatement():
+    n, T = 128, 3
+    ctx = oh.OceanContext(n, 1, T)
+    ctx.generate_noise_device(99)
+    ref = O.generate_noise_device(n, T, 99)
+    for t in range(T):
+        got = ctx.read(oh.TEX_NOISE, t)
+        assert np.abs(got - ref[t]).max() <= 1e-5  # logf ulp differences only; rejection path identical
+    g = ctx.read(oh.TEX_NOISE, 0).ravel().astype(np.float64)
+    assert abs(g.mean()) < 0.02 and abs(g.var() - 1.0) < 0.03
+    ctx.set_params(O.scene_params(), O.SCENE_CASCADES[:1])
+    ctx.init_spectrum()  # noise counts as set for every tile
+    ctx.step(0.1)
+    ctx.close()

@@ -217,3 +217,12 @@ def test_golden_fixtures_reproduce():
             if case["nplanes"] == 4:
                 np.testing.assert_array_equal(deriv, z[f"deriv_{f}"])
                 np.testing.assert_array_equal(turb, z[f"turb_{f}"])
+
+
+def test_device_noise_restatement_statistics():
+    g = O.generate_noise_device(64, 2, 7)
+    assert g.shape == (2, 64, 64, 2) and np.isfinite(g).all()
+    assert not np.array_equal(g[0], g[1])                     # tiles are independent streams
+    np.testing.assert_array_equal(g, O.generate_noise_device(64, 2, 7))  # deterministic
+    x = g.ravel().astype(np.float64)
+    assert abs(x.mean()) < 0.03 and abs(x.var() - 1.0) < 0.05
