@@ -33,7 +33,7 @@ constexpr int pa3_rows(int N, int RS = 2) { return N >= 1024 * RS ? 1 : 1024 * R
 // next item's h0 before this item's transform (its loads are then ahead of
 // this item's stores in the in-order vmcnt queue, so waiting for them never
 // waits for the stores); NOSTORE: timing experiment only (no output).
-template <int N, int P, int RS, bool PF, bool NOSTORE = false, bool NT = false>
+template <int N, int P, int RS, bool PF, bool NOSTORE = false>
 __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems) void k_pass_a3(DevView v, float time, int total_rows) {
     constexpr int RB = pa3_rows(N, RS);
     constexpr int FIRST = 16 / P;
@@ -102,9 +102,8 @@ __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems) void k_pass_a3(De
                 float2* rowp = v.tplane + (size_t)p * v.plane_stride + ((size_t)u2 * TILES * N + y2) * W;
                 if constexpr (NSL % W == 0) {
                     // x = jj + q*NSL: x/W = jj/W + q*NSL/W, x%W = jj%W (compile-time tile stride)
-                    float2* dst = rowp + (size_t)(jj / W) * N * W + (jj % W) + (size_t)q * (NSL / W) * N * W;
-                    if constexpr (NT) store2_nt(dst, val);
-                    else *dst = val;
+                    float2* dst = rowp + (size_t)(jj / W) * N * W + (jj % W);
+                    dst[(size_t)q * (NSL / W) * N * W] = val;
                 } else {
                     const int x = jj + q * NSL;
                     rowp[(size_t)(x / W) * N * W + (x % W)] = val;
@@ -125,7 +124,7 @@ __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems) void k_pass_a3(De
 
 // Pass B: one item = (unit, W-column tile); planes in the order DyDxz, DxDz,
 // DxxDzz, DyxDyz with the next PFD planes prefetched into registers.
-template <int N, int P, int PFD = 1, int NT = 1, bool XR = false>
+template <int N, int P, int PFD = 1>
 __global__ __launch_bounds__(b3_w(N) * N / kElems) void k_pass_b3(DevView v, int items) {
     using CT = ColTile<N, b3_w(N)>;
     using E = typename CT::E;
@@ -161,16 +160,14 @@ __global__ __launch_bounds__(b3_w(N) * N / kElems) void k_pass_b3(DevView v, int
     auto load = [&](int item, int p, float2 (&d)[kElems]) {
         const Win w = make_win(v.tplane + (size_t)p * v.plane_stride + (size_t)item * TILE, TILE * 8);
 #pragma unroll
-        for (int i = 0; i < kElems; ++i) d[i] = bload2<(NT & 4) ? 2 : 0>(w, toff * 8, CT::in_dy(i) * W * 8);
+        for (int i = 0; i < kElems; ++i) d[i] = bload2(w, toff * 8, CT::in_dy(i) * W * 8);
     };
 
     // PFD planes in flight ahead of the one being transformed (register ring)
     // (PFD = 0: no prefetch, each plane loaded when its step starts -- N = 4096,
     // where 1024 lanes leave 128 VGPRs)
     float2 cur[kElems], nxt[PFD > 0 ? kElems : 1], nx2[PFD > 1 ? kElems : 1];
-    // XR: adjacent tiles (which share 128-B output lines when W * 16 B < 128) on one XCD
-    int item = (XR && gridDim.x % 8 == 0) ? (int)(blockIdx.x % 8) * (int)(gridDim.x / 8) + (int)blockIdx.x / 8
-                                           : (int)blockIdx.x;
+    int item = blockIdx.x;
     if (item < items && PFD > 0) {
         load(item, order[0], cur);
         if constexpr (PFD > 1) load(item, order[1], nxt);
@@ -202,16 +199,11 @@ __global__ __launch_bounds__(b3_w(N) * N / kElems) void k_pass_b3(DevView v, int
                 else if (item + (int)gridDim.x < items) load(item + gridDim.x, order[0], nxt);
             }
             const Win wd = win16(v.disp, item), wt = win16(v.turb, item), wv = win16(v.deriv, item);
-            // NT bit 0: texture outputs streamed (nontemporal); bit 1: foam state too;
-            // bit 2: intermediate tile loads nontemporal
-            auto st4 = [&](float4 x, const Win& w, int voff, int soff) {
-                if constexpr (NT & 1) gstore4_nt(x, w, voff, soff);
-                else gstore4(x, w, voff, soff);
-            };
-            auto stf = [&](float* a, float x) {
-                if constexpr (NT & 2) store1_nt(a, x);
-                else *a = x;
-            };
+            // texture outputs are streamed (nontemporal): nothing in the frame reads them
+            // back, and default-policy stores would evict h0k, the intermediate and the
+            // foam state from the Infinity Cache before the next frame re-reads them
+            auto st4 = [&](float4 x, const Win& w, int voff, int soff) { gstore4_nt(x, w, voff, soff); };
+            auto stf = [&](float* a, float x) { *a = x; };
             auto emit = [&](int m, int q, float2 val) {
                 const int i = m * RL + q;
                 const int dy = CT::out_dy(m, q);
@@ -413,66 +405,42 @@ int grid3(K kernel, int threads, int items) {
     return items < g ? items : g;
 }
 
-template <int N, int P, int RS, bool PF, bool NOSTORE = false, bool NT = false>
+template <int N, int P, int RS, bool PF, bool NOSTORE = false>
 hipError_t go_a3k(const DevView& v, float t, hipStream_t s) {
     constexpr int RB = pa3_rows(N, RS);
     constexpr int T = RB * P * N / kElems;
     const int total = v.units * N;
     const int items = (total + RB - 1) / RB;
-    const int g = grid3(k_pass_a3<N, P, RS, PF, NOSTORE, NT>, T, items);
-    hipLaunchKernelGGL((k_pass_a3<N, P, RS, PF, NOSTORE, NT>), dim3(g), dim3(T), 0, s, v, t, total);
+    const int g = grid3(k_pass_a3<N, P, RS, PF, NOSTORE>, T, items);
+    hipLaunchKernelGGL((k_pass_a3<N, P, RS, PF, NOSTORE>), dim3(g), dim3(T), 0, s, v, t, total);
     return hipGetLastError();
 }
 
-// OCEAN_A3_VARIANT selects measured alternatives at N = 1024 (pass A).
+// N = 1024, 4 planes: 2 rows per workgroup (512 lanes) with the next item's h0
+// prefetched; other sizes: pa3_rows(N, 1) rows.  OCEAN_A3_VARIANT=11 is a timing
+// build without the intermediate stores (pass A).
 template <int N, int P>
 hipError_t go_a3(const DevView& v, float t, hipStream_t s) {
-    static const int variant = env_int("OCEAN_A3_VARIANT", 0);
-    if constexpr (N == 1024 && P == 4) {
-        switch (variant) {
-            case 1: return go_a3k<N, P, 1, false>(v, t, s);       // 1 row / WG, no prefetch
-            case 2: return go_a3k<N, P, 1, true>(v, t, s);        // 1 row / WG, prefetch
-            case 11: return go_a3k<N, P, 2, true, true>(v, t, s);  // timing only: no stores
-            case 3: return go_a3k<N, P, 2, true, false, true>(v, t, s);  // nontemporal intermediate stores
-            default: return go_a3k<N, P, 2, true>(v, t, s);       // 2 rows / WG (512 lanes), prefetch
-        }
-    }
-    if (variant == 11) return go_a3k<N, P, 1, false, true>(v, t, s);  // timing only: no stores
-    return go_a3k<N, P, 1, false>(v, t, s);
+    static const bool nostore = env_int("OCEAN_A3_VARIANT", 0) == 11;
+    if constexpr (N == 1024 && P == 4)
+        return nostore ? go_a3k<N, P, 2, true, true>(v, t, s) : go_a3k<N, P, 2, true>(v, t, s);
+    return nostore ? go_a3k<N, P, 1, false, true>(v, t, s) : go_a3k<N, P, 1, false>(v, t, s);
 }
 
-template <int N, int P, int PFD, int NT = 1, bool XR = false>
+template <int N, int P, int PFD>
 hipError_t go_b3k(const DevView& v, hipStream_t s) {
     constexpr int W = b3_w(N);
     constexpr int T = W * N / kElems;
     const int items = v.units * (N / W);
-    const int g = grid3(k_pass_b3<N, P, PFD, NT, XR>, T, items);
-    hipLaunchKernelGGL((k_pass_b3<N, P, PFD, NT, XR>), dim3(g), dim3(T), 0, s, v, items);
+    const int g = grid3(k_pass_b3<N, P, PFD>, T, items);
+    hipLaunchKernelGGL((k_pass_b3<N, P, PFD>), dim3(g), dim3(T), 0, s, v, items);
     return hipGetLastError();
 }
 
-// Two planes in flight at N = 1024 (one workgroup per CU, registers to spare):
-// -3..5 % pass-B time on MI355X; OCEAN_B3_PFD=1 restores one.
+// Two planes in flight at N = 1024 (one workgroup per CU, registers to spare).
 template <int N, int P>
 hipError_t go_b3(const DevView& v, hipStream_t s) {
-    static const int pfd = env_int("OCEAN_B3_PFD", 2);
-    static const int nt = env_int("OCEAN_B3_NT", 1);
-    if constexpr (N == 4096) {
-        static const int m4 = env_int("OCEAN_B4K", 0);
-        if (m4 == 1) return go_b3k<N, P, 0, 0, true>(v, s);
-        if (m4 == 2) return go_b3k<N, P, 0, 1, true>(v, s);
-        if (m4 == 3) return go_b3k<N, P, 0, 0, false>(v, s);
-        return go_b3k<N, P, 0>(v, s);
-    }
-    if constexpr (N == 1024) {
-        if (pfd > 1) {
-            if (nt == 0) return go_b3k<N, P, 2, 0>(v, s);
-            if (nt == 3) return go_b3k<N, P, 2, 3>(v, s);
-            if (nt == 5) return go_b3k<N, P, 2, 5>(v, s);
-            if (nt == 7) return go_b3k<N, P, 2, 7>(v, s);
-            return go_b3k<N, P, 2, 1>(v, s);
-        }
-    }
+    if constexpr (N == 1024) return go_b3k<N, P, 2>(v, s);
     return go_b3k<N, P, 1>(v, s);
 }
 
@@ -487,11 +455,6 @@ hipError_t go_a4(const DevView& v, float t, hipStream_t s) {
 }
 
 }  // namespace
-
-bool pass_v3_supported(int n) {
-    static const int big = env_int("OCEAN_V3_BIG", 1);  // 0: N > 1024 on the v2 kernels (A/B)
-    return n >= 16 && n <= (big ? 4096 : 1024);
-}
 
 bool pass_a4_supported(int n, int planes) { return n == 1024 && planes == 4; }
 
@@ -532,8 +495,6 @@ hipError_t launch_pass_b_v3(const DevView& v, hipStream_t s) {
         OCEAN_B3(256)
         OCEAN_B3(512)
         OCEAN_B3(1024)
-        OCEAN_B3(2048)
-        OCEAN_B3(4096)
     }
 #undef OCEAN_B3
     return hipErrorInvalidValue;

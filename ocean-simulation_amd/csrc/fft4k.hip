@@ -189,11 +189,6 @@ __global__ __launch_bounds__(kSeq * kL1 / kElems) void k_col4s2(DevView v, int i
     }
 }
 
-int env_int4(const char* name, int dflt) {
-    const char* e = std::getenv(name);
-    return e ? std::atoi(e) : dflt;
-}
-
 template <class K>
 int grid4(K kernel, int threads, int items) {
     int per_cu = 0, dev = 0, cus = 0;
@@ -225,7 +220,7 @@ hipError_t go_c2(const DevView& v, hipStream_t s) {
 
 }  // namespace
 
-bool pass_c4_supported(int n) { return (n == 2048 || n == 4096) && env_int4("OCEAN_C4", 1) != 0; }
+bool pass_c4_supported(int n) { return n == 2048 || n == 4096; }
 
 hipError_t launch_pass_c4(const DevView& v, hipStream_t s) {
     hipError_t e = hipErrorInvalidValue;

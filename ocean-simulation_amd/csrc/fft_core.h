@@ -1,6 +1,6 @@
 // Shared FFT building blocks for gfx950: in-register inverse DFTs of radix
 // 2/4/8/16, compile-time Stockham plan (radix-16 stages, remainder last) and
-// the LDS padding rule.  Included by fft.hip (v1 kernels) and fft2.hip (v2).
+// the LDS padding rule.  Included through fft_engine.h by every FFT kernel file.
 #pragma once
 
 #include <hip/hip_runtime.h>

@@ -1,6 +1,6 @@
-// FFT engine shared by fft2.hip and fft3.hip: memory-op helpers, per-stage
+// FFT engine shared by fft2.hip, fft3.hip and fft4k.hip: memory-op helpers, per-stage
 // twiddle tables, the LDS Stockham engine and the column-tile geometry.
-// See fft2.hip for the design notes.
+// DESIGN.md section 3 has the design notes.
 #pragma once
 
 #include <type_traits>
@@ -55,16 +55,10 @@ __device__ __forceinline__ void gstore4(float4 x, const Win& w, int voff, int so
 // 5.8 TB/s with default-policy stores -- the write stream stops evicting the
 // tile reads' lines.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void gstore4_nt(float4 x, const Win& w, int voff, int soff) {
     const f32x4 v = {x.x, x.y, x.z, x.w};
     __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(w.p + voff + soff));
 }
-__device__ __forceinline__ void store2_nt(float2* p, float2 x) {
-    const f32x2 v = {x.x, x.y};
-    __builtin_nontemporal_store(v, reinterpret_cast<f32x2*>(p));
-}
-__device__ __forceinline__ void store1_nt(float* p, float x) { __builtin_nontemporal_store(x, p); }
 __device__ __forceinline__ void store4_nt(float4* p, float4 x) {
     const f32x4 v = {x.x, x.y, x.z, x.w};
     __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));

@@ -50,7 +50,6 @@ struct ocean_ctx {
     int device = 0;
     int n = 0, logn = 0, C = 0, T = 0, P = 4;
     uint32_t flags = 0;
-    int variant = 2;  // kernel generation: 1 = fft.hip, 2 = fft2.hip (OCEAN_KERNEL_VARIANT)
     hipStream_t stream = nullptr;
     // device buffers
     float2* noise = nullptr;
@@ -249,7 +248,6 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
     c->flags = flags;
     c->P = (flags & OCEAN_F_DISPLACEMENT_ONLY) ? 2 : 4;
     c->noise_set.assign(n_tiles, false);
-    if (const char* kv = std::getenv("OCEAN_KERNEL_VARIANT")) c->variant = std::atoi(kv) == 1 ? 1 : 2;
     if (const char* ka = std::getenv("OCEAN_A4")) c->a4 = std::atoi(ka);
 
     auto alloc = [&](void** p, size_t bytes) -> bool {
@@ -271,7 +269,7 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
         ok = ok && alloc((void**)&c->turb, tex * U * 16);
         ok = ok && alloc((void**)&c->foam, tex * U * 4);
     }
-    if (ocean::pass_v3_supported(n)) ok = ok && alloc((void**)&c->tplane, tex * U * 8 * c->P);
+    ok = ok && alloc((void**)&c->tplane, tex * U * 8 * c->P);
     if (flags & OCEAN_F_NORMALS) ok = ok && alloc((void**)&c->normal, tex * U * 16);
     if (flags & OCEAN_F_MIPS) {
         for (int l = 1; (n >> l) >= 1; ++l) c->mip_chain += (size_t)(n >> l) * (n >> l);
@@ -423,19 +421,10 @@ int ocean_ifft2d(ocean_ctx* ctx, int plane_mask) {
         }
         int np = 1;  // run of consecutive planes: one launch per direction (planes are one allocation)
         while (p + np < 4 && (plane_mask & (1 << (p + np)))) ++np;
-        if (ctx->variant == 2) {
-            if (int r = timed(ctx, 0, [&] { return ocean::launch_ifft_rows_v2(v, p, np, ctx->stream); }, "ifft_rows"))
-                return r;
-            if (int r = timed(ctx, 1, [&] { return ocean::launch_ifft_cols_v2(v, p, np, ctx->stream); }, "ifft_cols"))
-                return r;
-        } else {
-            for (int q = p; q < p + np; ++q) {
-                if (int r = timed(ctx, 0, [&] { return ocean::launch_ifft_rows(v, q, ctx->stream); }, "ifft_rows"))
-                    return r;
-                if (int r = timed(ctx, 1, [&] { return ocean::launch_ifft_cols(v, q, ctx->stream); }, "ifft_cols"))
-                    return r;
-            }
-        }
+        if (int r = timed(ctx, 0, [&] { return ocean::launch_ifft_rows_v2(v, p, np, ctx->stream); }, "ifft_rows"))
+            return r;
+        if (int r = timed(ctx, 1, [&] { return ocean::launch_ifft_cols_v2(v, p, np, ctx->stream); }, "ifft_cols"))
+            return r;
         p += np;
     }
     return OCEAN_OK;
@@ -473,19 +462,17 @@ int ocean_step(ocean_ctx* ctx, float time) {
 
 namespace {
 int step_fused(ocean_ctx* ctx, float time) {
+    // pass A: mirror-pair rows (N = 1024, 4 planes, h0k valid) or per-texel rows;
+    // pass B: column tiles (N <= 1024) or the four-step column passes (N >= 2048)
     const ocean::DevView v = ctx->view();
-    const bool v3 = ctx->variant == 2 && ocean::pass_v3_supported(ctx->n);
     if (int r = timed(ctx, 0, [&] {
-            if (v3 && ctx->a4 && ctx->h0k_valid) return ocean::launch_pass_a_v4(v, time, ctx->stream);
-            return v3 ? ocean::launch_pass_a_v3(v, time, ctx->stream)
-                      : ctx->variant == 2 ? ocean::launch_pass_a_v2(v, time, ctx->stream)
-                                          : ocean::launch_pass_a(v, time, ctx->stream);
+            if (ctx->a4 && ctx->h0k_valid) return ocean::launch_pass_a_v4(v, time, ctx->stream);
+            return ocean::launch_pass_a_v3(v, time, ctx->stream);
         }, "pass_a"))
         return r;
     return timed(ctx, 1, [&] {
-        if (v3 && ocean::pass_c4_supported(ctx->n)) return ocean::launch_pass_c4(v, ctx->stream);
-        return v3 ? ocean::launch_pass_b_v3(v, ctx->stream)
-                  : ctx->variant == 2 ? ocean::launch_pass_b_v2(v, ctx->stream) : ocean::launch_pass_b(v, ctx->stream);
+        if (ocean::pass_c4_supported(ctx->n)) return ocean::launch_pass_c4(v, ctx->stream);
+        return ocean::launch_pass_b_v3(v, ctx->stream);
     }, "pass_b");
 }
 }  // namespace
@@ -689,15 +676,11 @@ int ocean_step_bytes(ocean_ctx* ctx, uint64_t* pass_a, uint64_t* pass_b) {
         // fill: P planes [+ foam state read + write] -> outputs
         a = tex * (32 + 8 * P + 16 * P);
         b = tex * (16 * P + 8 * P + (full ? 8 : 0) + outs);
-    } else if (ctx->variant == 2 && ocean::pass_v3_supported(ctx->n)) {
+    } else {
         const bool a4 = ctx->a4 && ctx->h0k_valid && ocean::pass_a4_supported(ctx->n, ctx->P);
         a = tex * ((a4 ? 8 : 16) + 8 * P);
         b = tex * (8 * P + (full ? 8 : 0) + outs);  // + foam state read and write
         if (ocean::pass_c4_supported(ctx->n)) b += tex * 16 * P;  // four-step: step 1 reads + writes the planes
-    } else {
-        // v1/v2 standard-layout passes: pass A also reads the wave data, pass B the TURB image
-        a = tex * (32 + 8 * P);
-        b = tex * (8 * P + (full ? 16 : 0) + outs);
     }
     *pass_a = a;
     *pass_b = b;

@@ -1,5 +1,5 @@
 // Internal declarations shared by the C-ABI layer (ocean_abi.cpp) and the HIP
-// kernel translation units (spectrum.hip, fft.hip).  Not part of the ABI.
+// kernel translation units (spectrum.hip, fft2/3/4k.hip, mips.hip).  Not part of the ABI.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -56,29 +56,17 @@ hipError_t launch_fill(const DevView& v, hipStream_t s);
 hipError_t launch_foam_import(const DevView& v, hipStream_t s);
 hipError_t launch_noise(const DevView& v, uint64_t seed, hipStream_t s);
 
-// fft.hip
-// Standalone operator (IFFT.InverseFastFourierTransform): in-place row pass and
-// column(+permute) pass over plane `p` of every unit.
-hipError_t launch_ifft_rows(const DevView& v, int p, hipStream_t s);
-hipError_t launch_ifft_cols(const DevView& v, int p, hipStream_t s);
-// Fused frame: pass A = evolve + row IFFT of every plane; pass B = column IFFT +
-// permute + fill/foam (+ normals).
-hipError_t launch_pass_a(const DevView& v, float t, hipStream_t s);
-hipError_t launch_pass_b(const DevView& v, hipStream_t s);
-
-// fft2.hip: persistent, software-pipelined versions of the same four launches.
-// Entries of the per-stage twiddle tables stored at tw + N + 128 (see fft2.hip StageTw).
+// fft2.hip: the operator IFFT (IFFT.InverseFastFourierTransform): persistent,
+// software-pipelined row and column(+permute) launches, in place.
+// Entries of the per-stage twiddle tables stored at tw + N + 128 (see fft_engine.h StageTw).
 size_t stage_twiddle_entries(int n);
-// v2 operator launches cover `np` consecutive planes p .. p+np-1 (one allocation) in one launch.
+// Each launch covers `np` consecutive planes p .. p+np-1 (one allocation).
 hipError_t launch_ifft_rows_v2(const DevView& v, int p, int np, hipStream_t s);
 hipError_t launch_ifft_cols_v2(const DevView& v, int p, int np, hipStream_t s);
-hipError_t launch_pass_a_v2(const DevView& v, float t, hipStream_t s);
-hipError_t launch_pass_b_v2(const DevView& v, hipStream_t s);
 
-// fft3.hip (N <= 1024): fused frame through the tile-major intermediate; the
-// row pass recomputes wave data and feeds evolve straight into a radix-4/8
-// first stage; the column pass reads contiguous tiles and the compact foam state.
-bool pass_v3_supported(int n);
+// fft3.hip: fused frame through the tile-major intermediate; the row pass
+// recomputes wave data and feeds evolve straight into a radix-4/8 first stage;
+// the column pass (N <= 1024) reads contiguous tiles and the compact foam state.
 hipError_t launch_pass_a_v3(const DevView& v, float t, hipStream_t s);
 hipError_t launch_pass_b_v3(const DevView& v, hipStream_t s);
 // mips.hip: box-filter mip chains of DERIV and TURB (OCEAN_F_MIPS)

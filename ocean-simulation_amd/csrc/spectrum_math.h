@@ -1,5 +1,5 @@
 // Per-texel spectrum arithmetic shared by the elementwise kernels (spectrum.hip)
-// and the fused frame kernels (fft.hip).  Every expression keeps the
+// and the fused row passes (fft3.hip).  Every expression keeps the
 // reference's fp32 operation order; the library is built with
 // -ffp-contract=off so no FMA contraction changes a rounding (the phase
 // omega*t at large t is sensitive to one ulp of omega).
