@@ -456,11 +456,15 @@ hipError_t go_a4(const DevView& v, float t, hipStream_t s) {
 
 }  // namespace
 
-bool pass_a4_supported(int n, int planes) { return n == 1024 && planes == 4; }
+bool pass_a4_supported(int n, int planes) {
+    static const int on = env_int("OCEAN_A4_SIZES", 3);  // bit 0: N = 1024, bit 1: N = 512
+    return planes == 4 && ((n == 1024 && (on & 1)) || (n == 512 && (on & 2)));
+}
 
 hipError_t launch_pass_a_v4(const DevView& v, float t, hipStream_t s) {
     if (!pass_a4_supported(v.n, v.planes) || !v.h0k) return hipErrorInvalidValue;
     static const int nostore = env_int("OCEAN_A4_NOSTORE", 0);
+    if (v.n == 512) return nostore ? go_a4<512, true>(v, t, s) : go_a4<512>(v, t, s);
     return nostore ? go_a4<1024, true>(v, t, s) : go_a4<1024>(v, t, s);
 }
 

@@ -349,11 +349,12 @@ def _ctx_with_env(env, n, cas, **kw):
                 os.environ[k] = v
 
 
-def test_mirror_pair_row_pass_bit_identical():
+@pytest.mark.parametrize("n", [512, 1024])
+def test_mirror_pair_row_pass_bit_identical(n):
     """Pass A4 (rows y and N - y per item, texel pairs k / -k sharing wave data and
     phase) against the per-texel v3 row pass: same arithmetic per texel and per
-    butterfly, so every output bit matches (cfg3 shape, 3 frames incl. foam)."""
-    n, cas = 1024, O.SCENE_CASCADES
+    butterfly, so every output bit matches (cfg3 / cfg4 shapes, 3 frames incl. foam)."""
+    cas = O.SCENE_CASCADES
     a, _ = _ctx_with_env({"OCEAN_A4": "1"}, n, cas)
     b, _ = _ctx_with_env({"OCEAN_A4": "0"}, n, cas)
     for t in (0.0, 0.5, 250.0):
