@@ -196,8 +196,11 @@ def main():
 
     units = tiles * C
     B = algorithmic_bytes(ctx)
-    a_us = 1e3 * ka_ms / max(ka_n, 1)
-    b_us = 1e3 * kb_ms / max(kb_n, 1)
+    # kernel time per step (a step may launch each pass once per unit chunk, ocean_abi.cpp
+    # chunk_units); bytes per step / time per step = bytes per launch / time per launch
+    a_us = 1e3 * ka_ms / args.steps
+    b_us = 1e3 * kb_ms / args.steps
+    launches_per_step = max(kb_n, 1) / args.steps
     dom, dom_us = ("pass_b", b_us) if b_us >= a_us else ("pass_a", a_us)
     if args.unfused:
         dom = "ifft_cols" if dom == "pass_b" else "ifft_rows"
@@ -266,7 +269,8 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic[0] if traffic else None,
                          "traffic_source": f"profiles/{traffic[1]}/pmc_summary.json" if traffic else None,
-                         "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_us": round(dom_us, 3)},
+                         "algorithmic_bytes_per_step": dom_bytes, "kernel_us_per_step": round(dom_us, 3),
+                         "launches_per_step": round(launches_per_step, 2)},
             "kernels_us": {"pass_a" if not args.unfused else "rows": round(a_us, 3),
                            "pass_b" if not args.unfused else "cols": round(b_us, 3)},
             "frame": {"algorithmic_bytes_per_gpu": B["frame"],

@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -57,6 +58,7 @@ struct ocean_ctx {
     float2* h0k = nullptr;   // h0.xy for the mirror-pair row pass (pass_a4_supported sizes)
     bool h0k_valid = false;  // h0k matches h0 (false after ocean_write(H0): .zw may then be arbitrary)
     int a4 = 1;              // OCEAN_A4=0 selects the v3 row pass
+    long chunk_mib = 192;    // OCEAN_CHUNK_MIB: intermediate MiB per unit chunk (step_fused)
     float4* waves = nullptr;
     float2* plane[4] = {nullptr, nullptr, nullptr, nullptr};
     float4* disp = nullptr;
@@ -249,6 +251,7 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
     c->P = (flags & OCEAN_F_DISPLACEMENT_ONLY) ? 2 : 4;
     c->noise_set.assign(n_tiles, false);
     if (const char* ka = std::getenv("OCEAN_A4")) c->a4 = std::atoi(ka);
+    if (const char* kc = std::getenv("OCEAN_CHUNK_MIB")) c->chunk_mib = std::atol(kc);
 
     auto alloc = [&](void** p, size_t bytes) -> bool {
         if (hipMalloc(p, bytes) != hipSuccess) return false;
@@ -461,19 +464,58 @@ int ocean_step(ocean_ctx* ctx, float time) {
 }
 
 namespace {
+// View of units [u0, u0 + nu) (u0 a multiple of C, so unit u's cascade is still u % C).
+ocean::DevView sub_view(const ocean::DevView& v, int u0, int nu) {
+    ocean::DevView s = v;
+    const size_t off = (size_t)u0 * v.n * v.n;
+    s.units = nu;
+    s.h0 = v.h0 + off;
+    s.waves = v.waves + off;
+    if (v.h0k) s.h0k = v.h0k + off;
+    s.tplane = v.tplane + off;  // plane_stride unchanged: planes stay U * N * N apart
+    if (v.foam) s.foam = v.foam + off;
+    s.disp = v.disp + off;
+    if (v.deriv) s.deriv = v.deriv + off;
+    if (v.turb) s.turb = v.turb + off;
+    if (v.normal) s.normal = v.normal + off;
+    return s;
+}
+
+// Units per chunk: a frame over many units runs pass A and pass B chunk by chunk so
+// that the intermediate pass B re-reads is still in the 256 MiB Infinity Cache
+// (OCEAN_CHUNK_MIB of intermediate per chunk, 0 = whole frame at once).  Measured on
+// cfg4's 1024 units at 512^2 (8 MiB each): 64 MiB 37.9k, 128 MiB 40.7k, 192 MiB 43.1k,
+// 256 MiB 38.4k, unchunked 40.7k tile-frames/s.
+int chunk_units(const ocean_ctx* ctx) {
+    const long mib = ctx->chunk_mib;
+    const int U = (int)ctx->units();
+    if (mib <= 0) return U;
+    const size_t per_unit = ctx->texels() * 8 * ctx->P;
+    int k = (int)(((size_t)mib << 20) / per_unit);
+    k -= k % ctx->C;
+    if (k < ctx->C) k = ctx->C;
+    return k >= U ? U : k;
+}
+
 int step_fused(ocean_ctx* ctx, float time) {
-    // pass A: mirror-pair rows (N = 1024, 4 planes, h0k valid) or per-texel rows;
-    // pass B: column tiles (N <= 1024) or the four-step column passes (N >= 2048)
+    // pass A: mirror-pair rows (N = 512, 1024 with 4 planes and h0k valid) or per-texel
+    // rows; pass B: column tiles (N <= 1024) or the four-step column passes (N >= 2048)
     const ocean::DevView v = ctx->view();
-    if (int r = timed(ctx, 0, [&] {
-            if (ctx->a4 && ctx->h0k_valid) return ocean::launch_pass_a_v4(v, time, ctx->stream);
-            return ocean::launch_pass_a_v3(v, time, ctx->stream);
-        }, "pass_a"))
-        return r;
-    return timed(ctx, 1, [&] {
-        if (ocean::pass_c4_supported(ctx->n)) return ocean::launch_pass_c4(v, ctx->stream);
-        return ocean::launch_pass_b_v3(v, ctx->stream);
-    }, "pass_b");
+    const int U = (int)ctx->units(), K = chunk_units(ctx);
+    for (int u0 = 0; u0 < U; u0 += K) {
+        const ocean::DevView c = (K >= U) ? v : sub_view(v, u0, std::min(K, U - u0));
+        if (int r = timed(ctx, 0, [&] {
+                if (ctx->a4 && ctx->h0k_valid) return ocean::launch_pass_a_v4(c, time, ctx->stream);
+                return ocean::launch_pass_a_v3(c, time, ctx->stream);
+            }, "pass_a"))
+            return r;
+        if (int r = timed(ctx, 1, [&] {
+                if (ocean::pass_c4_supported(ctx->n)) return ocean::launch_pass_c4(c, ctx->stream);
+                return ocean::launch_pass_b_v3(c, ctx->stream);
+            }, "pass_b"))
+            return r;
+    }
+    return OCEAN_OK;
 }
 }  // namespace
 

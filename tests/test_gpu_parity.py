@@ -489,3 +489,19 @@ def test_device_noise_matches_restatement():
     ctx.init_spectrum()  # noise counts as set for every tile
     ctx.step(0.1)
     ctx.close()
+
+
+def test_chunked_frame_equals_whole_frame():
+    """Many units: pass A / pass B run per unit chunk (Infinity-Cache-sized); results equal
+    the single-launch frame bit for bit."""
+    n, cas, T = 128, O.SCENE_CASCADES, 6
+    a = _ctx_with_env({"OCEAN_CHUNK_MIB": "1"}, n, cas, tiles=T)[0]   # 2 MiB per unit -> chunks of C units
+    b = _ctx_with_env({"OCEAN_CHUNK_MIB": "0"}, n, cas, tiles=T)[0]
+    for t in (0.5, 1.0):
+        a.step(t)
+        b.step(t)
+    for tile in range(T):
+        for tex in (oh.TEX_DISP, oh.TEX_DERIV, oh.TEX_TURB):
+            np.testing.assert_array_equal(a.read_all(tex, tile), b.read_all(tex, tile))
+    a.close()
+    b.close()
