@@ -1,23 +1,25 @@
-// v3 fused frame for N <= 1024 (BASELINE cfg2 / cfg3 / cfg4 sizes).
+// The fused frame: pass A (rows) and pass B (columns, N <= 1024) through a
+// column-tile-major intermediate.
 //
-// Pass A (k_pass_a3): evolve + row IFFT.  A workgroup owns RB = 1024/N
-//   consecutive rows and all P planes of them (256 lanes for P = 4).  The
-//   Stockham plan starts with radix R0 = 16/P so that in stage 0 one lane holds
-//   every plane of R0 texels: the lane evolves those texels
-//   (TimeDependentSpectrum.compute:20-47) and runs the first butterflies on
-//   the results in registers -- no LDS round trip for the evolve.  The wave
-//   data (kx, 1/|k|, kz, omega) is recomputed from (x, y, cascade) with the
-//   init kernel's own arithmetic (spectrum_math.h wave_data, bit-identical)
-//   instead of being read: 16 B/texel less HBM traffic.  Outputs go to the
-//   column-tile-major intermediate [p][u][x/W][y][W], W = col_tile(N)
-//   (64 B runs at N = 1024; 2-row workgroups that write 128 B runs measured
-//   slower: this pass is VALU/latency-bound, not store-bound).
-// Pass B (k_pass_b3): per W-column tile, column IFFT of each plane from one
-//   contiguous 8*W*N-byte block, permute, fill/foam epilogue; the foam state
-//   is a compact float in the same tile-major layout (4 B read + 4 B write
+// Pass A3 (k_pass_a3, every N): evolve + row IFFT.  A workgroup owns RB rows and
+//   all P planes of them.  The Stockham plan starts with radix R0 = 16/P so that
+//   in stage 0 one lane holds every plane of R0 texels: the lane evolves those
+//   texels (TimeDependentSpectrum.compute:20-47) and runs the first butterflies
+//   on the results in registers -- no LDS round trip for the evolve.  The wave
+//   data (kx, 1/|k|, kz, omega) is recomputed from (x, y, cascade) with the init
+//   kernel's own arithmetic (spectrum_math.h wave_data, bit-identical) instead
+//   of being read: 16 B/texel less HBM traffic.  Outputs go to the tile-major
+//   intermediate [p][u][x/W][y][W], W = inter_w(N).
+// Pass A4 (k_pass_a4, N = 512 / 1024 with 4 planes): the same per row pair
+//   (y, N - y), sharing wave data and exp(i omega t) between k and -k and
+//   reading h0 once through h0k (see the kernel).
+// Pass B3 (k_pass_b3, N <= 1024): per W-column tile, column IFFT of each plane
+//   from one contiguous 8*W*N-byte block, permute, fill/foam epilogue; the foam
+//   state is a compact float in the same tile-major layout (4 B read + 4 B write
 //   instead of a 16 B RGBA read), TURB is written as its broadcast image.
+//   N >= 2048: fft4k.hip.
 //
-// Bytes per texel-cascade (P = 4): pass A 16 (h0) + 32 (planes) = 48;
+// Bytes per texel-cascade (P = 4): pass A 16 (h0; 8 for A4) + 32 (planes);
 // pass B 32 (planes) + 4 + 4 (foam) + 48 (DISP, DERIV, TURB) = 88.
 #include <cstdlib>
 

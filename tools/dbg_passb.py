@@ -1,3 +1,6 @@
+"""Per-channel error report of the fused frame against the oracle for N = 16..1024 and
+1 / 4 cascades (GPU).  Used to localise the gfx950 buffer_store corruption that made the
+kernels use global stores (findings): the corrupted channels stand out."""
 import sys, os
 sys.path.insert(0, 'ocean-simulation_amd'); sys.path.insert(0, 'oracle')
 import numpy as np, torch, ocean_hip as oh, oracle as O
