@@ -6,11 +6,13 @@
 A "step" is one ocean frame: ocean_step(t) = evolve -> 2D IFFT of every plane
 -> fill/foam for every (tile, cascade) unit the rank owns (WaterBody.cs:180-193
 minus GenerateMips), inputs resident in HBM.  Multi-GPU: one process per GPU
-(torchrun), independent oceans (tiles) sharded across ranks -- no data-path
-collective exists; gloo carries only the start/stop barrier and
-the max-over-ranks of the elapsed time.  `value` = ocean-frames of the
-configured ocean (4 x 1024^2 cascades for cfg3) completed per second over all
-ranks.  Rank 0 prints ONE JSON line.
+(torchrun).  cfg2/cfg3 scale weakly (every rank runs its own ocean); cfg4 and
+cfg5 split one job (ocean_hip.shard.plan_shard: tile blocks for cfg4; cascades,
+then column bands for cfg5 -- at 8 GPUs each rank owns one 4096^2 cascade's half
+columns).  No data-path collective exists; gloo carries only the
+start/stop barrier and the max-over-ranks of the elapsed time.  `value` =
+ocean-frames of the configured job (4 x 1024^2 cascades for cfg3) completed per
+second over all ranks.  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -28,7 +30,7 @@ import torch  # noqa: E402  (import before ocean_hip: one HIP runtime per proces
 import torch.distributed as dist  # noqa: E402
 
 import ocean_hip as oh  # noqa: E402
-from ocean_hip.shard import reduce_timing, shard_tiles, tile_seed  # noqa: E402
+from ocean_hip.shard import plan_shard, reduce_timing, tile_seed  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md (chip-level parameters)
 
@@ -48,8 +50,8 @@ CONFIGS = {
                  desc="4 x 1024^2 cascades, displacement + derivatives + Jacobian foam"),
     "cfg4": dict(n=512, cascades=4, tiles=256, disp_only=False, per_rank=False,
                  desc="256 tiles x 4 x 512^2 cascades, sharded over ranks"),
-    "cfg5": dict(n=4096, cascades=4, tiles=1, disp_only=False, per_rank=True,
-                 desc="4 x 4096^2 cascades"),
+    "cfg5": dict(n=4096, cascades=4, tiles=1, disp_only=False, per_rank=False,
+                 desc="4 x 4096^2 cascades, split over ranks (cascades, then column bands)"),
 }
 
 
@@ -132,14 +134,20 @@ def main():
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
 
     cfg = CONFIGS[args.config]
-    n, C = cfg["n"], cfg["cascades"]
+    n = cfg["n"]
     if cfg["per_rank"]:
         # weak scaling: every rank runs its own ocean(s) (global tiles rank*T .. rank*T+T-1)
         tiles = cfg["tiles"]
         first = rank * tiles
+        casc0, C, x0, nx = 0, cfg["cascades"], 0, n
+        job_oceans = tiles * world
     else:
-        # the job's fixed batch of tiles split into contiguous blocks over the ranks
-        first, tiles = shard_tiles(cfg["tiles"], world, rank)
+        # strong scaling: the job's fixed oceans split over the ranks -- contiguous tile
+        # blocks (cfg4), or one ocean's cascades and then column bands (cfg5 on 8 GPUs:
+        # one cascade, half the columns per rank); no data exchange either way
+        sh = plan_shard(cfg["tiles"], cfg["cascades"], n, world, rank)
+        first, tiles, casc0, C, x0, nx = sh.tile0, sh.tiles, sh.casc0, sh.cascades, sh.x0, sh.nx
+        job_oceans = cfg["tiles"]
     flags = (oh.F_DISPLACEMENT_ONLY if cfg["disp_only"] else 0) | (oh.F_UNFUSED if args.unfused else 0)
 
     # one GPU per rank; more ranks than GPUs (a rehearsal of the N-rank path on a
@@ -147,8 +155,10 @@ def main():
     device = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(device)
     ctx = oh.OceanContext(n, C, tiles, flags, device=device)
-    ctx.set_params(SCENE_PARAMS, SCENE_CASCADES[:C])
-    ctx.generate_noise(tile_seed(20251121, first))
+    ctx.set_params(SCENE_PARAMS, SCENE_CASCADES[casc0:casc0 + C])
+    ctx.generate_noise(tile_seed(20251121, first))  # the reference shares one noise texture over cascades
+    if nx != n:
+        ctx.set_column_band(x0, nx)
     ctx.init_spectrum()
     ctx.synchronize()
 
@@ -191,7 +201,7 @@ def main():
     kb_ms, kb_n = ctx.kernel_stats(1)
     ctx.set_kernel_timing(False)
 
-    elapsed, total_tiles = reduce_timing(elapsed, tiles, world)
+    elapsed, _ = reduce_timing(elapsed, tiles, world)
     elapsed_ev, _ = reduce_timing(elapsed_ev, tiles, world)
 
     units = tiles * C
@@ -245,7 +255,7 @@ def main():
         cpu = cpu_baseline(cfg)
 
     if rank == 0:
-        frames = args.steps * total_tiles  # ocean-frames (one frame of one ocean = C cascades of N^2)
+        frames = args.steps * job_oceans  # ocean-frames (one frame of one ocean = all its cascades of N^2)
         value = frames / elapsed
         out = {
             "metric": "ocean-surface frames/sec (4x1024^2 cascades)" if args.config == "cfg3"
@@ -261,10 +271,12 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (scene parameters of Waves.unity, seeded noise 20251121+tile)",
-            "config": {"workload": f"{args.config}: {cfg['desc']}", "n": n, "cascades": C,
-                       "tiles_per_gpu": tiles, "tiles_total": total_tiles,
+            "config": {"workload": f"{args.config}: {cfg['desc']}", "n": n, "cascades": cfg["cascades"],
+                       "tiles_per_gpu": tiles, "tiles_total": job_oceans,
+                       "rank0_shard": {"cascades": [casc0, casc0 + C], "columns": [x0, x0 + nx]},
                        "schedule": "unfused" if args.unfused else "fused (pass A + pass B)",
-                       "parallelism": f"independent oceans sharded over {world} GPU(s), no collective"},
+                       "parallelism": f"{'independent oceans' if cfg['per_rank'] else 'one job split'} "
+                                      f"over {world} GPU(s), no collective"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic[0] if traffic else None,

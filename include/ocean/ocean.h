@@ -139,6 +139,20 @@ int ocean_init_spectrum(ocean_ctx *ctx);
  * OCEAN_F_UNFUSED selects the reference-shaped one (same results to rounding). */
 int ocean_step(ocean_ctx *ctx, float time);
 
+/* Column band for splitting one (tile, cascade) unit over several GPUs (SURVEY.md 8e,
+ * "units < GPUs", cfg5 = 4 cascades on 8 GPUs; no reference counterpart -- the
+ * reference runs every unit on one GPU).  After this call ocean_step computes the
+ * full row IFFT of every row (the rows are needed whole) but stores, column-transforms
+ * and fills only the columns x_begin <= x < x_begin + x_count of every slice: DISP,
+ * DERIV, TURB and NORMAL are written there, bit-identical to a whole-band context's
+ * texels, and the other columns are left as they are (zero after ocean_create).
+ * Two contexts with complementary bands (one per GPU) produce a cascade between them
+ * with no data exchange.  x_begin and x_count are multiples of g = min(N, max(16,
+ * 8192 / N)); (0, N) restores the whole band.  Needs the fused schedule (not
+ * OCEAN_F_UNFUSED) and no OCEAN_F_MIPS; the unfused stages (ocean_evolve,
+ * ocean_ifft2d, ocean_fill) ignore the band. */
+int ocean_set_column_band(ocean_ctx *ctx, int x_begin, int x_count);
+
 /* Replaces the TimeDependentSpectrum dispatch alone (WaterBody.cs:181-182;
  * TimeDependentSpectrum.compute:20-47): writes PLANE0..3 at `time`.  Async. */
 int ocean_evolve(ocean_ctx *ctx, float time);

@@ -34,8 +34,10 @@ constexpr int pa3_rows(int N, int RS = 2) { return N >= 1024 * RS ? 1 : 1024 * R
 // RS: row-sets per workgroup (RB = pa3_rows(N, RS) rows); PF: prefetch the
 // next item's h0 before this item's transform (its loads are then ahead of
 // this item's stores in the in-order vmcnt queue, so waiting for them never
-// waits for the stores); NOSTORE: timing experiment only (no output).
-template <int N, int P, int RS, bool PF, bool NOSTORE = false>
+// waits for the stores); NOSTORE: timing experiment only (no output); BAND: a
+// column band narrower than N (stores outside it skipped; a separate instance so
+// that the whole-band frame pays no per-store test).
+template <int N, int P, int RS, bool PF, bool NOSTORE = false, bool BAND = false>
 __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems) void k_pass_a3(DevView v, float time, int total_rows) {
     constexpr int RB = pa3_rows(N, RS);
     constexpr int FIRST = 16 / P;
@@ -99,7 +101,8 @@ __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems) void k_pass_a3(De
             E::template bj<E::RL>((int)threadIdx.x + m * T, b, jj);
             const int p = b / RB, r2 = b % RB;
             const int row2 = item * RB + r2;
-            if (row2 < total_rows) {
+            // column band: rows are transformed whole, only the band's columns stored
+            if (row2 < total_rows && (!BAND || (unsigned)(jj + q * NSL - v.x0) < (unsigned)v.nx)) {
                 const int u2 = row2 / N, y2 = row2 % N;
                 float2* rowp = v.tplane + (size_t)p * v.plane_stride + ((size_t)u2 * TILES * N + y2) * W;
                 if constexpr (NSL % W == 0) {
@@ -155,12 +158,15 @@ __global__ __launch_bounds__(b3_w(N) * N / kElems) void k_pass_b3(DevView v, int
         if constexpr (kKeepLds) return keep_lds[i * T + threadIdx.x];
         else return keep_reg[i];
     };
-    auto win16 = [&](const float4* base, int item) {
-        const int u = item / CT::tiles, x0 = (item % CT::tiles) * W;
+    // item -> full tile index u * tiles + tile over the column band's tiles
+    const int bt0 = v.x0 / W, bnt = v.nx / W;
+    auto full = [&](int item) { return (item / bnt) * CT::tiles + bt0 + item % bnt; };
+    auto win16 = [&](const float4* base, int ft) {
+        const int u = ft / CT::tiles, x0 = (ft % CT::tiles) * W;
         return make_win(base + (size_t)u * N * N + x0, (unsigned)((N * N - x0) * 16));
     };
     auto load = [&](int item, int p, float2 (&d)[kElems]) {
-        const Win w = make_win(v.tplane + (size_t)p * v.plane_stride + (size_t)item * TILE, TILE * 8);
+        const Win w = make_win(v.tplane + (size_t)p * v.plane_stride + (size_t)full(item) * TILE, TILE * 8);
 #pragma unroll
         for (int i = 0; i < kElems; ++i) d[i] = bload2(w, toff * 8, CT::in_dy(i) * W * 8);
     };
@@ -176,8 +182,9 @@ __global__ __launch_bounds__(b3_w(N) * N / kElems) void k_pass_b3(DevView v, int
     }
     __syncthreads();
     for (; item < items; item += gridDim.x) {
-        const int x0 = (item % CT::tiles) * W;
-        float* foam = v.foam + (size_t)item * TILE + toff;
+        const int ft = full(item);
+        const int x0 = (ft % CT::tiles) * W;
+        float* foam = v.foam + (size_t)ft * TILE + toff;
         float fb[kElems];
 #pragma unroll
         for (int pi = 0; pi < P; ++pi) {
@@ -185,7 +192,7 @@ __global__ __launch_bounds__(b3_w(N) * N / kElems) void k_pass_b3(DevView v, int
             // foam state for the DxxDzz plane: loaded one plane ahead and before that
             // step's tile prefetch, so waiting for it never waits for the prefetch
             if (pi + 1 < P && order[pi + 1] == 3) {
-                const Win rf = make_win(v.foam + (size_t)item * TILE, TILE * 4);
+                const Win rf = make_win(v.foam + (size_t)ft * TILE, TILE * 4);
 #pragma unroll
                 for (int m = 0; m < kElems / RL; ++m)
 #pragma unroll
@@ -200,7 +207,7 @@ __global__ __launch_bounds__(b3_w(N) * N / kElems) void k_pass_b3(DevView v, int
                 if (pi + 1 < P) load(item, order[pi + 1], nxt);
                 else if (item + (int)gridDim.x < items) load(item + gridDim.x, order[0], nxt);
             }
-            const Win wd = win16(v.disp, item), wt = win16(v.turb, item), wv = win16(v.deriv, item);
+            const Win wd = win16(v.disp, ft), wt = win16(v.turb, ft), wv = win16(v.deriv, ft);
             // texture outputs are streamed (nontemporal): nothing in the frame reads them
             // back, and default-policy stores would evict h0k, the intermediate and the
             // foam state from the Infinity Cache before the next frame re-reads them
@@ -224,7 +231,7 @@ __global__ __launch_bounds__(b3_w(N) * N / kElems) void k_pass_b3(DevView v, int
                 } else {  // DyxDyz: DERIV = (Dyx, Dyz, Dxx, Dzz), NORMAL
                     const float2 k = kget(i);
                     st4(make_float4(re, im, k.x, k.y), wv, voff16, so);
-                    if (v.normals) st4(normal_from_deriv(re, im, k.x, k.y), win16(v.normal, item), voff16, so);
+                    if (v.normals) st4(normal_from_deriv(re, im, k.x, k.y), win16(v.normal, ft), voff16, so);
                 }
             };
             E::run_regs(cur, lds, tws, emit);
@@ -249,7 +256,7 @@ __global__ __launch_bounds__(b3_w(N) * N / kElems) void k_pass_b3(DevView v, int
 // Lane j (N/4 lanes) holds stage-0 butterfly j of row y1 and butterfly
 // jm = (NJ - j) % NJ of row y2, whose texels are the mirrors of its own: two
 // radix-4 butterflies x 4 planes = 32 values per lane (Engine EL = 32).
-template <int N, bool NOSTORE = false>
+template <int N, bool NOSTORE = false, bool BAND = false>
 __global__ __launch_bounds__(N / 4) void k_pass_a4(DevView v, float time, int items_per_unit, int items) {
     constexpr int P = 4, R0 = 4, RB = 2, EL = 32;
     using TW = StageTw<N, R0>;
@@ -367,6 +374,7 @@ __global__ __launch_bounds__(N / 4) void k_pass_a4(DevView v, float time, int it
             }
             int b, jj;
             E::template bj<E::RL>((int)threadIdx.x + m * T, b, jj);
+            if (BAND && (unsigned)(jj + q * NSL - v.x0) >= (unsigned)v.nx) return;  // outside the column band
             const int p = b / RB, y = (b % RB) ? y2 : y1;
             float2* dst = v.tplane + (size_t)p * v.plane_stride + ((size_t)u * TILES * N + y) * W +
                           (size_t)(jj / W) * N * W + (jj % W);
@@ -407,14 +415,17 @@ int grid3(K kernel, int threads, int items) {
     return items < g ? items : g;
 }
 
-template <int N, int P, int RS, bool PF, bool NOSTORE = false>
+template <int N, int P, int RS, bool PF, bool NOSTORE = false, bool BAND = false>
 hipError_t go_a3k(const DevView& v, float t, hipStream_t s) {
+    if constexpr (!BAND && !NOSTORE) {
+        if (v.nx != N) return go_a3k<N, P, RS, PF, false, true>(v, t, s);
+    }
     constexpr int RB = pa3_rows(N, RS);
     constexpr int T = RB * P * N / kElems;
     const int total = v.units * N;
     const int items = (total + RB - 1) / RB;
-    const int g = grid3(k_pass_a3<N, P, RS, PF, NOSTORE>, T, items);
-    hipLaunchKernelGGL((k_pass_a3<N, P, RS, PF, NOSTORE>), dim3(g), dim3(T), 0, s, v, t, total);
+    const int g = grid3(k_pass_a3<N, P, RS, PF, NOSTORE, BAND>, T, items);
+    hipLaunchKernelGGL((k_pass_a3<N, P, RS, PF, NOSTORE, BAND>), dim3(g), dim3(T), 0, s, v, t, total);
     return hipGetLastError();
 }
 
@@ -433,7 +444,7 @@ template <int N, int P, int PFD>
 hipError_t go_b3k(const DevView& v, hipStream_t s) {
     constexpr int W = b3_w(N);
     constexpr int T = W * N / kElems;
-    const int items = v.units * (N / W);
+    const int items = v.units * (v.nx / W);
     const int g = grid3(k_pass_b3<N, P, PFD>, T, items);
     hipLaunchKernelGGL((k_pass_b3<N, P, PFD>), dim3(g), dim3(T), 0, s, v, items);
     return hipGetLastError();
@@ -446,13 +457,16 @@ hipError_t go_b3(const DevView& v, hipStream_t s) {
     return go_b3k<N, P, 1>(v, s);
 }
 
-template <int N, bool NOSTORE = false>
+template <int N, bool NOSTORE = false, bool BAND = false>
 hipError_t go_a4(const DevView& v, float t, hipStream_t s) {
+    if constexpr (!BAND && !NOSTORE) {
+        if (v.nx != N) return go_a4<N, false, true>(v, t, s);
+    }
     constexpr int T = N / 4;
     const int ipu = N / 2;
     const int items = v.units * ipu;
-    const int g = grid3(k_pass_a4<N, NOSTORE>, T, items);
-    hipLaunchKernelGGL((k_pass_a4<N, NOSTORE>), dim3(g), dim3(T), 0, s, v, t, ipu, items);
+    const int g = grid3(k_pass_a4<N, NOSTORE, BAND>, T, items);
+    hipLaunchKernelGGL((k_pass_a4<N, NOSTORE, BAND>), dim3(g), dim3(T), 0, s, v, t, ipu, items);
     return hipGetLastError();
 }
 

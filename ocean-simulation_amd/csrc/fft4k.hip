@@ -71,9 +71,11 @@ __global__ __launch_bounds__(kSeq * (N / kL1) / kElems) void k_col4s1(DevView v,
     for (int i = threadIdx.x; i < 128; i += T) two[i] = v.tw[N + i];
     const int lb = (int)threadIdx.x % kSeq, lj = (int)threadIdx.x / kSeq;
     const int tiles = N / kWT;
+    const int bt0 = v.x0 / kWT, bnt = v.nx / kWT;  // column band's tiles
     auto base_of = [&](int item) {
-        const int blk = item % BLKS, rest = item / BLKS;  // rest = (p * units + u) * tiles + tile
-        const int p = rest / (v.units * tiles), ut = rest % (v.units * tiles);
+        const int blk = item % BLKS, rest = item / BLKS;  // rest = (p * units + u) * band tiles + band tile
+        const int p = rest / (v.units * bnt), ub = rest % (v.units * bnt);
+        const int ut = (ub / bnt) * tiles + bt0 + ub % bnt;
         return v.tplane + (size_t)p * v.plane_stride + (size_t)ut * TILE + blk * (kSeq / kWT) * kWT;
     };
     float2 cur[kElems], nxt[kElems];
@@ -128,8 +130,10 @@ __global__ __launch_bounds__(kSeq * kL1 / kElems) void k_col4s2(DevView v, int i
     const int tiles = N / kWT;
     auto kput = [&](int i, float2 x) { keep[i * T + threadIdx.x] = x; };
     auto kget = [&](int i) { return keep[i * T + threadIdx.x]; };
+    const int bt0 = v.x0 / kWT, bnt = v.nx / kWT;  // column band's tiles
+    auto full = [&](int ub) { return (ub / bnt) * tiles + bt0 + ub % bnt; };
     auto load = [&](int item, int p, float2 (&d)[kElems]) {
-        const int blk = item % BLKS, ut = item / BLKS;
+        const int blk = item % BLKS, ut = full(item / BLKS);
         const float2* src = v.tplane + (size_t)p * v.plane_stride + (size_t)ut * TILE +
                             (size_t)kL1 * (blk * K0B + k0l) * kWT + col + lj * kWT;
 #pragma unroll
@@ -140,7 +144,7 @@ __global__ __launch_bounds__(kSeq * kL1 / kElems) void k_col4s2(DevView v, int i
     if (item < items) load(item, order[0], cur);
     __syncthreads();
     for (; item < items; item += gridDim.x) {
-        const int blk = item % BLKS, ut = item / BLKS;
+        const int blk = item % BLKS, ut = full(item / BLKS);
         const int u = ut / tiles, tile = ut % tiles;
         const int k0 = blk * K0B + k0l, x = tile * kWT + col;
         const int y0 = k0 + L0 * lj;  // lane's first output row; element (m, q) adds L0 * out_dy
@@ -203,7 +207,7 @@ int grid4(K kernel, int threads, int items) {
 template <int N>
 hipError_t go_c1(const DevView& v, hipStream_t s) {
     constexpr int T = kSeq * (N / kL1) / kElems;
-    const int items = v.planes * v.units * (N / kWT) * (kL1 / (kSeq / kWT));
+    const int items = v.planes * v.units * (v.nx / kWT) * (kL1 / (kSeq / kWT));
     const int g = grid4(k_col4s1<N>, T, items);
     hipLaunchKernelGGL((k_col4s1<N>), dim3(g), dim3(T), 0, s, v, items);
     return hipGetLastError();
@@ -212,7 +216,7 @@ hipError_t go_c1(const DevView& v, hipStream_t s) {
 template <int N, int P>
 hipError_t go_c2(const DevView& v, hipStream_t s) {
     constexpr int T = kSeq * kL1 / kElems;
-    const int items = v.units * (N / kWT) * ((N / kL1) / (kSeq / kWT));
+    const int items = v.units * (v.nx / kWT) * ((N / kL1) / (kSeq / kWT));
     const int g = grid4(k_col4s2<N, P>, T, items);
     hipLaunchKernelGGL((k_col4s2<N, P>), dim3(g), dim3(T), 0, s, v, items);
     return hipGetLastError();

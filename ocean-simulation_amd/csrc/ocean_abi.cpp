@@ -59,6 +59,7 @@ struct ocean_ctx {
     bool h0k_valid = false;  // h0k matches h0 (false after ocean_write(H0): .zw may then be arbitrary)
     int a4 = 1;              // OCEAN_A4=0 selects the v3 row pass
     long chunk_mib = 192;    // OCEAN_CHUNK_MIB: intermediate MiB per unit chunk (step_fused)
+    int band_x0 = 0, band_nx = 0;  // column band of the fused passes (ocean_set_column_band); nx = n: whole
     float4* waves = nullptr;
     float2* plane[4] = {nullptr, nullptr, nullptr, nullptr};
     float4* disp = nullptr;
@@ -116,6 +117,8 @@ struct ocean_ctx {
         v.deriv_mips = deriv_mips;
         v.turb_mips = turb_mips;
         v.mip_chain = mip_chain;
+        v.x0 = band_x0;
+        v.nx = band_nx;
         return v;
     }
 
@@ -250,6 +253,7 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
     c->flags = flags;
     c->P = (flags & OCEAN_F_DISPLACEMENT_ONLY) ? 2 : 4;
     c->noise_set.assign(n_tiles, false);
+    c->band_nx = n;
     if (const char* ka = std::getenv("OCEAN_A4")) c->a4 = std::atoi(ka);
     if (const char* kc = std::getenv("OCEAN_CHUNK_MIB")) c->chunk_mib = std::atol(kc);
 
@@ -692,6 +696,21 @@ int ocean_synchronize(ocean_ctx* ctx) {
     return OCEAN_OK;
 }
 
+int ocean_set_column_band(ocean_ctx* ctx, int x_begin, int x_count) {
+    if (int r = enter(ctx)) return r;
+    const int n = ctx->n;
+    const int g = std::min(n, std::max(16, 8192 / n));  // a multiple of every tile width of the fused passes
+    if (x_begin < 0 || x_count < 1 || x_begin + x_count > n || x_begin % g || x_count % g)
+        return fail(OCEAN_E_INVALID_ARG, "column band [" + std::to_string(x_begin) + ", +" + std::to_string(x_count) +
+                                             ") must lie in [0, N) with start and width multiples of " +
+                                             std::to_string(g));
+    if (x_count != n && (ctx->flags & (OCEAN_F_UNFUSED | OCEAN_F_MIPS)))
+        return fail(OCEAN_E_UNSUPPORTED, "a column band needs the fused schedule and no mip chains");
+    ctx->band_x0 = x_begin;
+    ctx->band_nx = x_count;
+    return OCEAN_OK;
+}
+
 int ocean_set_kernel_timing(ocean_ctx* ctx, int enable) {
     if (int r = enter(ctx)) return r;
     if (enable && ctx->event_pool.size() < 4096) {
@@ -720,9 +739,11 @@ int ocean_step_bytes(ocean_ctx* ctx, uint64_t* pass_a, uint64_t* pass_b) {
         b = tex * (16 * P + 8 * P + (full ? 8 : 0) + outs);
     } else {
         const bool a4 = ctx->a4 && ctx->h0k_valid && ocean::pass_a4_supported(ctx->n, ctx->P);
-        a = tex * ((a4 ? 8 : 16) + 8 * P);
-        b = tex * (8 * P + (full ? 8 : 0) + outs);  // + foam state read and write
-        if (ocean::pass_c4_supported(ctx->n)) b += tex * 16 * P;  // four-step: step 1 reads + writes the planes
+        // column band: h0 is read whole (rows are transformed whole), the rest scales with the band
+        const uint64_t bt = tex / ctx->n * ctx->band_nx;
+        a = tex * (a4 ? 8 : 16) + bt * 8 * P;
+        b = bt * (8 * P + (full ? 8 : 0) + outs);  // + foam state read and write
+        if (ocean::pass_c4_supported(ctx->n)) b += bt * 16 * P;  // four-step: step 1 reads + writes the planes
     }
     *pass_a = a;
     *pass_b = b;

@@ -42,6 +42,10 @@ struct DevView {
     float4* deriv_mips;   // OCEAN_F_MIPS: per slice, levels 1..log2 N concatenated (mip_chain texels)
     float4* turb_mips;
     size_t mip_chain;     // texels per slice chain: sum over L >= 1 of (N >> L)^2
+    // column band (ocean_set_column_band): the fused passes store / transform / fill
+    // columns x0 <= x < x0 + nx only (rows are still transformed whole); x0 and nx are
+    // multiples of the tile widths, full band = (0, N)
+    int x0, nx;
 };
 
 struct SpectrumParams {

@@ -60,7 +60,7 @@ EXPORTED_SYMBOLS = (
     "ocean_write", "ocean_get_device_ptr", "ocean_get_stream", "ocean_synchronize",
     "ocean_set_kernel_timing", "ocean_kernel_stats", "ocean_step_bytes", "ocean_read_mip", "ocean_get_mip_ptr",
     "ocean_generate_noise_device", "ocean_read_async", "ocean_readback_status", "ocean_readback_wait", "ocean_readback_release",
-    "ocean_host_alloc", "ocean_host_free", "ocean_last_error", "ocean_abi_version",
+    "ocean_host_alloc", "ocean_host_free", "ocean_last_error", "ocean_abi_version", "ocean_set_column_band",
 )
 
 
@@ -124,6 +124,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "ocean_host_free": ([P], None),
         "ocean_last_error": ([], ctypes.c_char_p),
         "ocean_abi_version": ([], i),
+        "ocean_set_column_band": ([P, i, i], i),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -252,6 +253,11 @@ class OceanContext:
         s = ctypes.c_void_p()
         _check(self.lib.ocean_get_stream(self._h, ctypes.byref(s)), "ocean_get_stream")
         return s.value or 0
+
+    def set_column_band(self, x_begin: int, x_count: int) -> None:
+        """Restrict the fused step's stores, column transforms and fill to columns
+        [x_begin, x_begin + x_count) (one GPU's share of a unit split over several)."""
+        _check(self.lib.ocean_set_column_band(self._h, x_begin, x_count), "ocean_set_column_band")
 
     # -- timing ---------------------------------------------------------------
     def set_kernel_timing(self, enable: bool) -> None:

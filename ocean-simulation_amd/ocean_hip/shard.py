@@ -1,4 +1,5 @@
-"""Multi-GPU sharding of independent oceans.
+"""Multi-GPU sharding of independent oceans, and of one ocean's
+cascades and column bands when there are more GPUs than (tile, cascade) units.
 
 The per-frame path has no exchange step: every (tile, cascade) unit's
 spectrum -> IFFT -> outputs -> foam chain touches only its own data.  Tiles
@@ -9,6 +10,7 @@ barrier and the max-over-ranks of the elapsed time in bench.py.
 """
 from __future__ import annotations
 
+from dataclasses import dataclass
 from typing import Tuple
 
 
@@ -20,6 +22,55 @@ def shard_tiles(total_tiles: int, world: int, rank: int) -> Tuple[int, int]:
     count = base + (1 if rank < extra else 0)
     first = rank * base + min(rank, extra)
     return first, count
+
+
+@dataclass(frozen=True)
+class Shard:
+    """One rank's share of a job of `tiles` oceans x C cascades at N^2: global tiles
+    [tile0, tile0 + tiles), cascades [casc0, casc0 + cascades) of each, and the column
+    band [x0, x0 + nx) of each of those slices (ocean_set_column_band)."""
+    tile0: int
+    tiles: int
+    casc0: int
+    cascades: int
+    x0: int
+    nx: int
+
+
+def band_granularity(n: int) -> int:
+    """Column-band start/width granularity of ocean_set_column_band at N = n."""
+    return min(n, max(16, 8192 // n))
+
+
+def plan_shard(total_tiles: int, n_cascades: int, n: int, world: int, rank: int) -> Shard:
+    """Split a job over `world` GPUs with no data exchange.
+
+    world <= tiles: contiguous tile blocks, every cascade, whole slices (cfg4).
+    Otherwise each tile gets s = world / tiles ranks (world a multiple of tiles):
+    s <= C: the tile's cascades in contiguous blocks (cfg5 at 2 and 4 GPUs);
+    s > C (s a multiple of C): each cascade split into b = s / C column bands of
+    N / b columns (cfg5 at 8 GPUs: one cascade, half the columns per GPU).  A band
+    rank still runs the full row IFFT of its cascade (rows are needed whole)."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("bad world/rank")
+    if world <= total_tiles:
+        t0, nt = shard_tiles(total_tiles, world, rank)
+        return Shard(t0, nt, 0, n_cascades, 0, n)
+    if world % total_tiles:
+        raise ValueError(f"{world} ranks over {total_tiles} tiles: world must be a multiple of the tile count")
+    s = world // total_tiles
+    tile, r = divmod(rank, s)
+    if s <= n_cascades:
+        c0, nc = shard_tiles(n_cascades, s, r)
+        return Shard(tile, 1, c0, nc, 0, n)
+    if s % n_cascades:
+        raise ValueError(f"{s} ranks per tile over {n_cascades} cascades: must be a multiple")
+    b = s // n_cascades
+    c, k = divmod(r, b)
+    width = n // b
+    if width < band_granularity(n) or width % band_granularity(n):
+        raise ValueError(f"{b} column bands of N = {n} are narrower than the band granularity")
+    return Shard(tile, 1, c, 1, k * width, width)
 
 
 def tile_seed(seed: int, global_tile: int) -> int:

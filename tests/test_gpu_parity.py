@@ -505,3 +505,80 @@ def test_chunked_frame_equals_whole_frame():
             np.testing.assert_array_equal(a.read_all(tex, tile), b.read_all(tex, tile))
     a.close()
     b.close()
+
+
+# ------------------------------------------------- cascade subsets + column bands
+@pytest.mark.parametrize("n,ncasc,world", [(256, 2, 4), (512, 4, 8), (1024, 4, 8), (4096, 2, 4)])
+def test_split_ocean_shards_bit_identical(n, ncasc, world):
+    """One ocean split over `world` GPUs by ocean_hip.shard.plan_shard (cascade blocks,
+    then column bands: cfg5's 8-GPU split at world = 2 x cascades), each shard its own
+    context here on one GPU: every texel of every shard equals the whole ocean's bit for
+    bit (the same arithmetic per texel; no data exchange), and columns outside a shard's
+    band stay untouched (zero).  N = 512 / 1024 run the mirror-pair row pass, 4096 the
+    four-step column passes."""
+    from ocean_hip.shard import plan_shard
+    cas = O.SCENE_CASCADES[:ncasc]
+    whole, _ = make_ctx(n, cas)
+    shards = []
+    for r in range(world):
+        sh = plan_shard(1, ncasc, n, world, r)
+        ctx, _ = make_ctx(n, cas[sh.casc0:sh.casc0 + sh.cascades])
+        ctx.set_column_band(sh.x0, sh.nx)
+        shards.append((sh, ctx))
+    assert any(sh.nx < n for sh, _ in shards)
+    for t in (0.25, 3.0):
+        whole.step(t)
+        for _, ctx in shards:
+            ctx.step(t)
+    for tex in (oh.TEX_DISP, oh.TEX_DERIV, oh.TEX_TURB):
+        ref = whole.read_all(tex)
+        for sh, ctx in shards:
+            got = ctx.read_all(tex)
+            band = slice(sh.x0, sh.x0 + sh.nx)
+            np.testing.assert_array_equal(got[..., band, :], ref[sh.casc0:sh.casc0 + sh.cascades, :, band, :],
+                                          err_msg=f"tex {tex} shard {sh}")
+            outside = np.ones(n, bool)
+            outside[band] = False
+            assert not got[..., outside, :].any(), f"tex {tex} shard {sh} wrote outside its band"
+    whole.close()
+    for _, ctx in shards:
+        ctx.close()
+
+
+def test_column_band_narrow_and_restored():
+    """A 16-column band at an interior offset (N = 1024, tiles of 8), then the whole band
+    again: the band context's next frames match the whole-band context everywhere (foam
+    of the columns outside the band restarted from its frozen state is not compared)."""
+    n, cas = 1024, O.SCENE_CASCADES[:1]
+    a, _ = make_ctx(n, cas)
+    b, _ = make_ctx(n, cas)
+    b.set_column_band(496, 16)
+    a.step(0.5)
+    b.step(0.5)
+    np.testing.assert_array_equal(b.read(oh.TEX_DISP)[:, 496:512], a.read(oh.TEX_DISP)[:, 496:512])
+    b.set_column_band(0, n)
+    a.step(1.0)
+    b.step(1.0)
+    np.testing.assert_array_equal(b.read(oh.TEX_DISP), a.read(oh.TEX_DISP))
+    np.testing.assert_array_equal(b.read(oh.TEX_DERIV), a.read(oh.TEX_DERIV))
+    a.close()
+    b.close()
+
+
+def test_column_band_errors_and_bytes():
+    n, cas = 1024, O.SCENE_CASCADES
+    ctx, _ = make_ctx(n, cas)
+    for x0, nx in ((8, 16), (0, 8), (0, 0), (1024 - 16, 32), (-16, 16)):
+        with pytest.raises(oh.OceanError) as e:
+            ctx.set_column_band(x0, nx)
+        assert e.value.code == oh.E_INVALID_ARG
+    tex = n * n * len(cas)
+    ctx.set_column_band(512, 512)
+    assert ctx.step_bytes() == (8 * tex + 16 * tex, 44 * tex)  # h0k read whole, the rest halves
+    ctx.close()
+    u, _ = make_ctx(256, cas[:1], flags=oh.F_UNFUSED)
+    with pytest.raises(oh.OceanError) as e:
+        u.set_column_band(0, 128)
+    assert e.value.code == oh.E_UNSUPPORTED
+    u.set_column_band(0, 256)  # the whole band is always allowed
+    u.close()
