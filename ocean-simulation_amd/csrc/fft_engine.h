@@ -8,6 +8,10 @@
 #include "fft_core.h"
 #include "ocean_internal.h"
 
+#ifndef OCEAN_NO_WAVE_PRIVATE
+#define OCEAN_NO_WAVE_PRIVATE 0  // 1: workgroup barriers between all stages (A/B builds)
+#endif
+
 namespace ocean {
 namespace {
 using namespace fftcore;
@@ -234,6 +238,22 @@ struct Engine {
     }
     static_assert(!(PAD && SEQ_FAST) || seq_pad_ok(), "column-tile padding needs 16-row-aligned strides");
     static constexpr bool linear() { return true; }
+    // Stages st.. are wave-private when every one of them has N / R = 64 butterflies
+    // per sequence on row-major lanes: lane g = tid + m * THREADS then works on sequence
+    // g / 64, so each wave reads and writes only its own sequences (the same ones at
+    // every such stage) and the stages need no workgroup barrier -- LDS operations of
+    // one wave execute in order; a compiler fence keeps them in program order.
+    static constexpr bool wave_private(int st) {
+        if (SEQ_FAST || OCEAN_NO_WAVE_PRIVATE) return false;
+        for (int s = st; s < S; ++s)
+            if (N / radix_of(N, s, FIRST) != 64) return false;
+        return st < S;
+    }
+    template <int ST>
+    static __device__ __forceinline__ void stage_sync() {
+        if constexpr (wave_private(ST)) __asm__ volatile("" ::: "memory");
+        else __syncthreads();
+    }
 
     // Stages ST.. from LDS; the last stage hands (m, q, value) to emit.
     template <int ST, class Emit>
@@ -258,7 +278,7 @@ struct Engine {
                 for (int r = 0; r < R; ++r) v[m * R + r] = lds[lidx(b, j + r * (N / R))];
             }
         }
-        if constexpr (!LAST) __syncthreads();
+        if constexpr (!LAST) stage_sync<ST>();
 #pragma unroll
         for (int m = 0; m < BF; ++m) {
             int b, j;
@@ -281,7 +301,7 @@ struct Engine {
             }
         }
         if constexpr (!LAST) {
-            __syncthreads();
+            stage_sync<ST>();
             stages_from<ST + 1>(lds, tws, emit);
         }
     }
