@@ -83,7 +83,7 @@ __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems) void k_pass_a3(De
         // stage-0 inputs: plane m of texel x = j + r*NJ of row (item*RB + rr)
         const int row = item * RB + rr;
         const int u = row / N, y = row % N;
-        const WaveBand wb = band[u % v.C];
+        const WaveBand wb = band[(u + v.c0) % v.C];
         float2 in[kElems];
 #pragma unroll
         for (int r = 0; r < R0; ++r) {
@@ -304,7 +304,7 @@ __global__ __launch_bounds__(N / 4) void k_pass_a4(DevView v, float time, int it
         if (next < items) load_pair(next, An, Bn);
         int u, y1, y2;
         rows_of(item, u, y1, y2);
-        const WaveBand wb = band[u % v.C];
+        const WaveBand wb = band[(u + v.c0) % v.C];
         float2 in[EL];  // slot (s*4 + p)*4 + r: set s (row y1 / y2), plane p, stage-0 input r
         if (y1 != 0) {
             float2 mir[P][R0];  // set-2 values in mirror order (slot r = mirror of set-1 slot r)

@@ -59,6 +59,8 @@ struct ocean_ctx {
     bool h0k_valid = false;  // h0k matches h0 (false after ocean_write(H0): .zw may then be arbitrary)
     int a4 = 1;              // OCEAN_A4=0 selects the v3 row pass
     long chunk_mib = 192;    // OCEAN_CHUNK_MIB: intermediate MiB per unit chunk (step_fused)
+    int c4_bands = 0;        // OCEAN_C4_BANDS: N >= 2048 column passes per (unit, band); 0 = auto
+    int chunk_min = 1 << 30; // OCEAN_CHUNK_MIN: units per chunk when one unit exceeds OCEAN_CHUNK_MIB
     int band_x0 = 0, band_nx = 0;  // column band of the fused passes (ocean_set_column_band); nx = n: whole
     float4* waves = nullptr;
     float2* plane[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -256,6 +258,8 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
     c->band_nx = n;
     if (const char* ka = std::getenv("OCEAN_A4")) c->a4 = std::atoi(ka);
     if (const char* kc = std::getenv("OCEAN_CHUNK_MIB")) c->chunk_mib = std::atol(kc);
+    if (const char* kb = std::getenv("OCEAN_C4_BANDS")) c->c4_bands = std::max(0, std::atoi(kb));
+    if (const char* km = std::getenv("OCEAN_CHUNK_MIN")) c->chunk_min = std::max(1, std::atoi(km));
 
     auto alloc = [&](void** p, size_t bytes) -> bool {
         if (hipMalloc(p, bytes) != hipSuccess) return false;
@@ -468,11 +472,12 @@ int ocean_step(ocean_ctx* ctx, float time) {
 }
 
 namespace {
-// View of units [u0, u0 + nu) (u0 a multiple of C, so unit u's cascade is still u % C).
+// View of units [u0, u0 + nu) (unit u of the view is cascade (c0 + u) % C).
 ocean::DevView sub_view(const ocean::DevView& v, int u0, int nu) {
     ocean::DevView s = v;
     const size_t off = (size_t)u0 * v.n * v.n;
     s.units = nu;
+    s.c0 = (v.c0 + u0) % v.C;
     s.h0 = v.h0 + off;
     s.waves = v.waves + off;
     if (v.h0k) s.h0k = v.h0k + off;
@@ -496,9 +501,25 @@ int chunk_units(const ocean_ctx* ctx) {
     if (mib <= 0) return U;
     const size_t per_unit = ctx->texels() * 8 * ctx->P;
     int k = (int)(((size_t)mib << 20) / per_unit);
-    k -= k % ctx->C;
-    if (k < ctx->C) k = ctx->C;
+    if (k >= ctx->C) k -= k % ctx->C;  // whole tiles when a chunk holds one
+    if (k < 1) k = ctx->chunk_min;
     return k >= U ? U : k;
+}
+
+// Column bands per unit for the N >= 2048 column passes: OCEAN_C4_BANDS, or by default
+// as many as keep one band's planes (P * N * width * 8 B) within 256 MiB -- cfg5's 512 MiB
+// units run as 2 bands: 387 -> 412-421 frames/s (3 or 4 bands: 417; per-unit pass A: slower).
+// Band widths stay multiples of the four-step tile width (16).
+int c4_bands(const ocean_ctx* ctx, int nx) {
+    if (!ocean::pass_c4_supported(ctx->n)) return 1;
+    int nb = ctx->c4_bands;
+    if (nb <= 0) {
+        const size_t band_bytes = (size_t)ctx->P * ctx->n * nx * 8;
+        nb = 1;
+        while (band_bytes / nb > ((size_t)256 << 20)) nb *= 2;
+    }
+    while (nb > 1 && (nx % nb || (nx / nb) % 16)) --nb;
+    return nb;
 }
 
 int step_fused(ocean_ctx* ctx, float time) {
@@ -513,6 +534,21 @@ int step_fused(ocean_ctx* ctx, float time) {
                 return ocean::launch_pass_a_v3(c, time, ctx->stream);
             }, "pass_a"))
             return r;
+        const int nb = c4_bands(ctx, c.nx);
+        if (nb > 1) {
+            // four-step column passes per (unit, column band): pass C2 re-reads what C1
+            // just wrote while it is still in the Infinity Cache (256 MiB)
+            const int w = c.nx / nb;
+            for (int u = 0; u < c.units; ++u)
+                for (int b = 0; b < nb; ++b) {
+                    ocean::DevView cb = sub_view(c, u, 1);
+                    cb.x0 = c.x0 + b * w;
+                    cb.nx = (b == nb - 1) ? c.nx - b * w : w;
+                    if (int r = timed(ctx, 1, [&] { return ocean::launch_pass_c4(cb, ctx->stream); }, "pass_c"))
+                        return r;
+                }
+            continue;
+        }
         if (int r = timed(ctx, 1, [&] {
                 if (ocean::pass_c4_supported(ctx->n)) return ocean::launch_pass_c4(c, ctx->stream);
                 return ocean::launch_pass_b_v3(c, ctx->stream);

@@ -46,6 +46,7 @@ struct DevView {
     // columns x0 <= x < x0 + nx only (rows are still transformed whole); x0 and nx are
     // multiples of the tile widths, full band = (0, N)
     int x0, nx;
+    int c0;  // cascade of unit 0 of this view (a sub-view of a unit chunk may start mid-tile)
 };
 
 struct SpectrumParams {

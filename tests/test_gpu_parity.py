@@ -582,3 +582,20 @@ def test_column_band_errors_and_bytes():
     assert e.value.code == oh.E_UNSUPPORTED
     u.set_column_band(0, 256)  # the whole band is always allowed
     u.close()
+
+
+@pytest.mark.parametrize("n,bands", [(2048, "4"), (4096, "0")])
+def test_four_step_column_bands_bit_identical(n, bands):
+    """N >= 2048: the column passes C1 + C2 run per (unit, column band) so that C2 re-reads
+    C1's output from the Infinity Cache (OCEAN_C4_BANDS; 0 = auto, 2 bands at 4096).  The
+    per-texel arithmetic is unchanged: bit-identical to one launch pair over everything."""
+    cas = O.SCENE_CASCADES[:2] if n == 2048 else O.SCENE_CASCADES[:1]
+    a, _ = _ctx_with_env({"OCEAN_C4_BANDS": "1"}, n, cas)
+    b, _ = _ctx_with_env({"OCEAN_C4_BANDS": bands}, n, cas)
+    for t in (0.5, 2.0):
+        a.step(t)
+        b.step(t)
+    for tex in (oh.TEX_DISP, oh.TEX_DERIV, oh.TEX_TURB):
+        np.testing.assert_array_equal(a.read_all(tex), b.read_all(tex))
+    a.close()
+    b.close()
