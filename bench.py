@@ -106,11 +106,29 @@ def cpu_baseline(cfg, frames=3):
     scale = (n * n * np.log2(n)) / (n_s * n_s * np.log2(n_s))
     sec *= scale
     per_tile = 1.0 / sec
+    # secondary figure (Parallel.For over the host cores): the same frames on
+    # the box's CPU share -- OMP_NUM_THREADS (16 per GPU on the GPU pool), else the cores
+    threads = int(os.environ.get("OMP_NUM_THREADS") or min(16, os.cpu_count() or 1))
+    multi = None
+    if threads > 1:
+        O.set_threads(threads)
+        try:
+            oc.step(0.5)  # warm-up (thread pool start)
+            tm = []
+            for f in range(frames):
+                t0 = time.perf_counter()
+                oc.step((f + 1) / 30.0)
+                tm.append(time.perf_counter() - t0)
+        finally:
+            O.set_threads(1)
+        multi = {"value": 1.0 / (float(np.median(tm)) * scale), "cores": threads,
+                 "sample": f"median of {frames} frames, OpenMP over the oracle's frame loops"}
     return {"value": per_tile, "unit": "frames/s", "cores": 1, "kind": "port",
             "sample": f"median of {frames} frames after 1 warm-up, 1 ocean of {C} x {n_s}^2 "
                       f"{'(scaled x%.2f to %d^2) ' % (scale, n) if scale != 1 else ''}"
                       f"on 1 host core; C port of the reference path (oracle/ocean_oracle.c); "
-                      f"the C# scalar baseline of north_star needs dotnet, absent on this image"}
+                      f"the C# scalar baseline of north_star needs dotnet, absent on this image",
+            "multicore": multi}
 
 
 def main():

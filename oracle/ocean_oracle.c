@@ -236,12 +236,21 @@ void oracle_conjugate_spectrum(int n, int ncasc, float *h0) {
 
 /* ------------------------------------------------------------------------ */
 /* Time-dependent spectrum: TimeDependentSpectrum.compute:16-47              */
+/* ------------------------------------------------------------------------ */
+/* Threads for the per-frame loops (evolve, IFFT stages, permute, fill): 1 by
+ * default, the scalar restatement the tests check against.  bench.py's
+ * cpu_baseline also times a multi-core run; every element of every stage is
+ * still computed by the same expression from the previous stage's buffer, so
+ * the result does not depend on the thread count. */
+static int or_nthreads = 1;
+void oracle_set_threads(int n) { or_nthreads = n < 1 ? 1 : n; }
 /* planes[4]: each float2[C][N][N]: DxDz, DyDxz, DyxDyz, DxxDzz (:42-45).     */
 /* ------------------------------------------------------------------------ */
 void oracle_evolve(int n, int ncasc, const float *h0, const float *waves, float t, float *p0, float *p1, float *p2,
                    float *p3) {
-    size_t cnt = (size_t)ncasc * n * n;
-    for (size_t i = 0; i < cnt; i++) {
+    long cnt = (long)ncasc * n * n;
+#pragma omp parallel for num_threads(or_nthreads) schedule(static) if (or_nthreads > 1)
+    for (long i = 0; i < cnt; i++) {
         const float *w = waves + i * 4;
         const float *h = h0 + i * 4;
         float phase = w[3] * t;
@@ -297,6 +306,7 @@ void oracle_ifft2d(int n, int ncasc, const float *table, float *input, float *pi
         for (int s = 0; s < logn; s++) {
             const float *src = pp ? pingpong : input;
             float *dst = pp ? input : pingpong;
+#pragma omp parallel for collapse(2) num_threads(or_nthreads) schedule(static) if (or_nthreads > 1)
             for (int c = 0; c < ncasc; c++)
                 for (int y = 0; y < n; y++)
                     for (int x = 0; x < n; x++) {
@@ -321,6 +331,7 @@ void oracle_ifft2d(int n, int ncasc, const float *table, float *input, float *pi
         }
     }
     /* 2*log2N passes: even, so the result is back in `input`. Permute (:73-78). */
+#pragma omp parallel for collapse(2) num_threads(or_nthreads) schedule(static) if (or_nthreads > 1)
     for (int c = 0; c < ncasc; c++)
         for (int y = 0; y < n; y++)
             for (int x = 0; x < n; x++) {
@@ -338,8 +349,9 @@ void oracle_ifft2d(int n, int ncasc, const float *table, float *input, float *pi
 
 void oracle_fill(int n, int ncasc, const float *p0, const float *p1, const float *p2, const float *p3, float *disp,
                  float *deriv, float *turb) {
-    size_t cnt = (size_t)ncasc * n * n;
-    for (size_t i = 0; i < cnt; i++) {
+    long cnt = (long)ncasc * n * n;
+#pragma omp parallel for num_threads(or_nthreads) schedule(static) if (or_nthreads > 1)
+    for (long i = 0; i < cnt; i++) {
         disp[i * 4 + 0] = p0[i * 2 + 0];
         disp[i * 4 + 1] = p1[i * 2 + 0];
         disp[i * 4 + 2] = p0[i * 2 + 1];

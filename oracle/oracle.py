@@ -59,11 +59,18 @@ def lib():
         L.oracle_ifft2d.argtypes = [i, i, fp, fp, fp]
         L.oracle_fill.argtypes = [i, i, fp, fp, fp, fp, fp, fp, fp]
         L.oracle_step.argtypes = [i, i, i, fp, fp, fp, f, fp, fp, fp, fp, fp]
+        L.oracle_set_threads.argtypes = [i]
         for fn in (L.oracle_generate_noise, L.oracle_init_spectrum, L.oracle_conjugate_spectrum, L.oracle_evolve,
-                   L.oracle_twiddle_table, L.oracle_ifft2d, L.oracle_fill, L.oracle_step):
+                   L.oracle_twiddle_table, L.oracle_ifft2d, L.oracle_fill, L.oracle_step, L.oracle_set_threads):
             fn.restype = None
         _lib = L
     return _lib
+
+
+def set_threads(n: int) -> None:
+    """Threads of the per-frame loops (evolve, IFFT stages, fill); 1 (the default) is the
+    scalar restatement.  Results do not depend on it (element-wise stages)."""
+    lib().oracle_set_threads(int(n))
 
 
 def _p(a):

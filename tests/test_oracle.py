@@ -226,3 +226,23 @@ def test_device_noise_restatement_statistics():
     np.testing.assert_array_equal(g, O.generate_noise_device(64, 2, 7))  # deterministic
     x = g.ravel().astype(np.float64)
     assert abs(x.mean()) < 0.03 and abs(x.var() - 1.0) < 0.05
+
+
+def test_threaded_oracle_frames_identical():
+    """bench.py's multi-core CPU baseline runs the oracle's frame loops on several threads;
+    every stage is element-wise over the previous stage's buffer, so the frames are
+    bit-identical to the scalar run."""
+    n, cas = 64, O.SCENE_CASCADES
+    noise = O.generate_noise(n, 99)
+    a = O.OracleOcean(n, O.scene_params(), cas, noise)
+    b = O.OracleOcean(n, O.scene_params(), cas, noise)
+    try:
+        for t in (0.0, 0.7, 40.0):
+            ra = [x.copy() for x in a.step(t)]
+            O.set_threads(4)
+            rb = b.step(t)
+            O.set_threads(1)
+            for x, y in zip(ra, rb):
+                np.testing.assert_array_equal(x, y)
+    finally:
+        O.set_threads(1)
