@@ -186,10 +186,12 @@ def test_golden_fixtures(flags):
 
 
 @pytest.mark.parametrize("n,ncasc,flags", [(256, 1, 0), (512, 1, oh.F_DISPLACEMENT_ONLY), (512, 3, 0),
-                                           (1024, 4, 0), (1024, 4, oh.F_UNFUSED), (2048, 1, 0)])
+                                           (1024, 4, 0), (1024, 4, oh.F_UNFUSED), (2048, 1, 0),
+                                           (4096, 1, 0), (4096, 1, oh.F_DISPLACEMENT_ONLY)])
 def test_frames_vs_oracle(n, ncasc, flags):
     """BASELINE configs: cfg1-shaped 256^2 x1, cfg2 512^2 displacement only, the scene (512^2 x3),
-    cfg3 4 x 1024^2 full outputs; 3 frames so the foam state is exercised."""
+    cfg3 4 x 1024^2 full outputs, and one cfg5 cascade at 4096^2 (four-step column passes, the
+    radix-2 oracle at full size); 3 frames so the foam state is exercised."""
     cas = O.SCENE_CASCADES[:ncasc]
     ctx, (noise,) = make_ctx(n, cas, flags=flags)
     nplanes = 2 if flags & oh.F_DISPLACEMENT_ONLY else 4
