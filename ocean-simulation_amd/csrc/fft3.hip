@@ -256,11 +256,17 @@ __global__ __launch_bounds__(b3_w(N) * N / kElems) void k_pass_b3(DevView v, int
 // Lane j (N/4 lanes) holds stage-0 butterfly j of row y1 and butterfly
 // jm = (NJ - j) % NJ of row y2, whose texels are the mirrors of its own: two
 // radix-4 butterflies x 4 planes = 32 values per lane (Engine EL = 32).
-template <int N, bool NOSTORE = false, bool BAND = false>
+//
+// PH: planes per LDS pass.  PH = 2 (default) holds 4 of the 8 sequences in LDS (planes
+// p0, p0 + 1 of both rows) and runs the stages twice per item: 43.5 KiB of LDS instead of
+// 78 KiB, so 3 workgroups share a CU instead of 2 and the per-workgroup latency chain
+// (evolve -> LDS stages -> stores) overlaps better: 38.6 -> 33.0 us at cfg3.
+template <int N, bool NOSTORE = false, bool BAND = false, int PH = 2>
 __global__ __launch_bounds__(N / 4) void k_pass_a4(DevView v, float time, int items_per_unit, int items) {
     constexpr int P = 4, R0 = 4, RB = 2, EL = 32;
+    static_assert(PH == 2 || PH == 4, "stages need 16 values per lane");
     using TW = StageTw<N, R0>;
-    using E = Engine<N, RB * P, false, true, R0, TW, EL>;
+    using E = Engine<N, RB * PH, false, true, R0, TW, EL * PH / P>;
     constexpr int T = E::THREADS;
     constexpr int NJ = N / R0;
     static_assert(T == NJ && E::R0 == R0, "lane j <-> stage-0 butterfly j");
@@ -356,37 +362,42 @@ __global__ __launch_bounds__(N / 4) void k_pass_a4(DevView v, float time, int it
                 }
             }
         }
-        // stage 0 (radix 4) in registers; sequence b = p * 2 + s
+        // stage 0 (radix 4) in registers; LDS sequence b = (p - p0) * 2 + s
         const int jb1 = (y1 != 0) ? jm : j;
 #pragma unroll
-        for (int g = 0; g < 2 * P; ++g) {
-            Idft<R0>::run(&in[g * R0]);
-            const int s = g / P, p = g % P;
-            float2* dst = lds + E::lidx(p * RB + s, (s ? jb1 : j) * R0);
+        for (int g = 0; g < 2 * P; ++g) Idft<R0>::run(&in[g * R0]);
 #pragma unroll
-            for (int q = 0; q < R0; ++q) dst[E::loff(q, 1)] = in[g * R0 + q];
-        }
-        __syncthreads();
-        auto emit = [&](int m, int q, float2 val) {
-            if constexpr (NOSTORE) {
-                asm volatile("" ::"v"(val.x), "v"(val.y));
-                return;
+        for (int p0 = 0; p0 < P; p0 += PH) {
+#pragma unroll
+            for (int g = 0; g < 2 * P; ++g) {
+                const int s = g / P, p = g % P;
+                if (p < p0 || p >= p0 + PH) continue;
+                float2* dst = lds + E::lidx((p - p0) * RB + s, (s ? jb1 : j) * R0);
+#pragma unroll
+                for (int q = 0; q < R0; ++q) dst[E::loff(q, 1)] = in[g * R0 + q];
             }
-            int b, jj;
-            E::template bj<E::RL>((int)threadIdx.x + m * T, b, jj);
-            if (BAND && (unsigned)(jj + q * NSL - v.x0) >= (unsigned)v.nx) return;  // outside the column band
-            const int p = b / RB, y = (b % RB) ? y2 : y1;
-            float2* dst = v.tplane + (size_t)p * v.plane_stride + ((size_t)u * TILES * N + y) * W +
-                          (size_t)(jj / W) * N * W + (jj % W);
-            dst[(size_t)q * (NSL / W) * N * W] = val;
-        };
-        E::template stages_from<1>(lds, tws, emit);
+            __syncthreads();
+            auto emit = [&](int m, int q, float2 val) {
+                if constexpr (NOSTORE) {
+                    asm volatile("" ::"v"(val.x), "v"(val.y));
+                    return;
+                }
+                int b, jj;
+                E::template bj<E::RL>((int)threadIdx.x + m * T, b, jj);
+                if (BAND && (unsigned)(jj + q * NSL - v.x0) >= (unsigned)v.nx) return;  // outside the column band
+                const int p = p0 + b / RB, y = (b % RB) ? y2 : y1;
+                float2* dst = v.tplane + (size_t)p * v.plane_stride + ((size_t)u * TILES * N + y) * W +
+                              (size_t)(jj / W) * N * W + (jj % W);
+                dst[(size_t)q * (NSL / W) * N * W] = val;
+            };
+            E::template stages_from<1>(lds, tws, emit);
+            __syncthreads();
+        }
 #pragma unroll
         for (int r = 0; r < R0; ++r) {
             A[r] = An[r];
             B[r] = Bn[r];
         }
-        __syncthreads();
     }
 }
 
@@ -457,16 +468,16 @@ hipError_t go_b3(const DevView& v, hipStream_t s) {
     return go_b3k<N, P, 1>(v, s);
 }
 
-template <int N, bool NOSTORE = false, bool BAND = false>
+template <int N, bool NOSTORE = false, bool BAND = false, int PH = 2>
 hipError_t go_a4(const DevView& v, float t, hipStream_t s) {
     if constexpr (!BAND && !NOSTORE) {
-        if (v.nx != N) return go_a4<N, false, true>(v, t, s);
+        if (v.nx != N) return go_a4<N, false, true, PH>(v, t, s);
     }
     constexpr int T = N / 4;
     const int ipu = N / 2;
     const int items = v.units * ipu;
-    const int g = grid3(k_pass_a4<N, NOSTORE, BAND>, T, items);
-    hipLaunchKernelGGL((k_pass_a4<N, NOSTORE, BAND>), dim3(g), dim3(T), 0, s, v, t, ipu, items);
+    const int g = grid3(k_pass_a4<N, NOSTORE, BAND, PH>, T, items);
+    hipLaunchKernelGGL((k_pass_a4<N, NOSTORE, BAND, PH>), dim3(g), dim3(T), 0, s, v, t, ipu, items);
     return hipGetLastError();
 }
 
@@ -480,7 +491,12 @@ bool pass_a4_supported(int n, int planes) {
 hipError_t launch_pass_a_v4(const DevView& v, float t, hipStream_t s) {
     if (!pass_a4_supported(v.n, v.planes) || !v.h0k) return hipErrorInvalidValue;
     static const int nostore = env_int("OCEAN_A4_NOSTORE", 0);
-    if (v.n == 512) return nostore ? go_a4<512, true>(v, t, s) : go_a4<512>(v, t, s);
+    static const int whole = env_int("OCEAN_A4_WHOLE", 0);  // 1: all 4 planes in one LDS pass (A/B)
+    if (v.n == 512) {
+        if (whole) return go_a4<512, false, false, 4>(v, t, s);
+        return nostore ? go_a4<512, true>(v, t, s) : go_a4<512>(v, t, s);
+    }
+    if (whole) return go_a4<1024, false, false, 4>(v, t, s);
     return nostore ? go_a4<1024, true>(v, t, s) : go_a4<1024>(v, t, s);
 }
 
