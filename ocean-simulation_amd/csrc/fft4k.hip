@@ -194,10 +194,11 @@ __global__ __launch_bounds__(kSeq * kL1 / kElems) void k_col4s2(DevView v, int i
 }
 
 template <class K>
-int grid4(K kernel, int threads, int items) {
+int grid4(K kernel, int threads, int items, int max_per_cu = 0) {
     int per_cu = 0, dev = 0, cus = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0) != hipSuccess || per_cu <= 0)
         per_cu = 1;
+    if (max_per_cu > 0 && per_cu > max_per_cu) per_cu = max_per_cu;
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
     const int g = cus * per_cu;
@@ -208,7 +209,9 @@ template <int N>
 hipError_t go_c1(const DevView& v, hipStream_t s) {
     constexpr int T = kSeq * (N / kL1) / kElems;
     const int items = v.planes * v.units * (v.nx / kWT) * (kL1 / (kSeq / kWT));
-    const int g = grid4(k_col4s1<N>, T, items);
+    // two workgroups per CU, not the four that fit: cfg5 column passes 1.72 -> 1.67 ms
+    // (three per CU: 1.70 ms), DESIGN.md section 3
+    const int g = grid4(k_col4s1<N>, T, items, 2);
     hipLaunchKernelGGL((k_col4s1<N>), dim3(g), dim3(T), 0, s, v, items);
     return hipGetLastError();
 }
