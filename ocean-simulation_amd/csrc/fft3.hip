@@ -37,7 +37,7 @@ constexpr int pa3_rows(int N, int RS = 2) { return N >= 1024 * RS ? 1 : 1024 * R
 // waits for the stores); NOSTORE: timing experiment only (no output); BAND: a
 // column band narrower than N (stores outside it skipped; a separate instance so
 // that the whole-band frame pays no per-store test).
-template <int N, int P, int RS, bool PF, bool NOSTORE = false, bool BAND = false>
+template <int N, int P, int RS, bool PF, bool NOSTORE = false, bool BAND = false, int WT = 0>
 __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems) void k_pass_a3(DevView v, float time, int total_rows) {
     constexpr int RB = pa3_rows(N, RS);
     constexpr int FIRST = 16 / P;
@@ -46,7 +46,7 @@ __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems) void k_pass_a3(De
     constexpr int T = E::THREADS;
     constexpr int R0 = E::R0;             // = FIRST (texels per lane)
     constexpr int NJ = N / R0;            // stage-0 butterflies per sequence
-    constexpr int W = inter_w(N);
+    constexpr int W = WT ? WT : inter_w(N);  // WT: narrow tiles of a small job (ocean_create)
     constexpr int TILES = N / W;
     constexpr int NSL = N / E::RL;        // last-stage Ns
     static_assert(T / NJ == RB, "stage-0 mapping: lane -> (row, j), butterfly m -> plane m");
@@ -129,9 +129,9 @@ __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems) void k_pass_a3(De
 
 // Pass B: one item = (unit, W-column tile); planes in the order DyDxz, DxDz,
 // DxxDzz, DyxDyz with the next PFD planes prefetched into registers.
-template <int N, int P, int PFD = 1>
-__global__ __launch_bounds__(b3_w(N) * N / kElems) void k_pass_b3(DevView v, int items) {
-    using CT = ColTile<N, b3_w(N)>;
+template <int N, int P, int PFD = 1, int WT = 0>
+__global__ __launch_bounds__((WT ? WT : b3_w(N)) * N / kElems) void k_pass_b3(DevView v, int items) {
+    using CT = ColTile<N, WT ? WT : b3_w(N)>;
     using E = typename CT::E;
     using TW = typename CT::TW;
     constexpr int W = CT::W;
@@ -261,7 +261,7 @@ __global__ __launch_bounds__(b3_w(N) * N / kElems) void k_pass_b3(DevView v, int
 // p0, p0 + 1 of both rows) and runs the stages twice per item: 43.5 KiB of LDS instead of
 // 78 KiB, so 3 workgroups share a CU instead of 2 and the per-workgroup latency chain
 // (evolve -> LDS stages -> stores) overlaps better: 38.6 -> 33.0 us at cfg3.
-template <int N, bool NOSTORE = false, bool BAND = false, int PH = 2>
+template <int N, bool NOSTORE = false, bool BAND = false, int PH = 2, int WT = 0>
 __global__ __launch_bounds__(N / 4) void k_pass_a4(DevView v, float time, int items_per_unit, int items) {
     constexpr int P = 4, R0 = 4, RB = 2, EL = 32;
     static_assert(PH == 2 || PH == 4, "stages need 16 values per lane");
@@ -270,7 +270,7 @@ __global__ __launch_bounds__(N / 4) void k_pass_a4(DevView v, float time, int it
     constexpr int T = E::THREADS;
     constexpr int NJ = N / R0;
     static_assert(T == NJ && E::R0 == R0, "lane j <-> stage-0 butterfly j");
-    constexpr int W = inter_w(N);
+    constexpr int W = WT ? WT : inter_w(N);
     constexpr int TILES = N / W;
     constexpr int NSL = N / E::RL;
     static_assert(NSL % W == 0, "tile-major emit");
@@ -426,17 +426,20 @@ int grid3(K kernel, int threads, int items) {
     return items < g ? items : g;
 }
 
-template <int N, int P, int RS, bool PF, bool NOSTORE = false, bool BAND = false>
+template <int N, int P, int RS, bool PF, bool NOSTORE = false, bool BAND = false, int WT = 0>
 hipError_t go_a3k(const DevView& v, float t, hipStream_t s) {
+    if constexpr (WT == 0 && N >= 128 && N <= 1024) {
+        if (v.tile_w != inter_w(N)) return go_a3k<N, P, RS, PF, NOSTORE, BAND, 4>(v, t, s);
+    }
     if constexpr (!BAND && !NOSTORE) {
-        if (v.nx != N) return go_a3k<N, P, RS, PF, false, true>(v, t, s);
+        if (v.nx != N) return go_a3k<N, P, RS, PF, false, true, WT>(v, t, s);
     }
     constexpr int RB = pa3_rows(N, RS);
     constexpr int T = RB * P * N / kElems;
     const int total = v.units * N;
     const int items = (total + RB - 1) / RB;
-    const int g = grid3(k_pass_a3<N, P, RS, PF, NOSTORE, BAND>, T, items);
-    hipLaunchKernelGGL((k_pass_a3<N, P, RS, PF, NOSTORE, BAND>), dim3(g), dim3(T), 0, s, v, t, total);
+    const int g = grid3(k_pass_a3<N, P, RS, PF, NOSTORE, BAND, WT>, T, items);
+    hipLaunchKernelGGL((k_pass_a3<N, P, RS, PF, NOSTORE, BAND, WT>), dim3(g), dim3(T), 0, s, v, t, total);
     return hipGetLastError();
 }
 
@@ -451,13 +454,16 @@ hipError_t go_a3(const DevView& v, float t, hipStream_t s) {
     return nostore ? go_a3k<N, P, 1, false, true>(v, t, s) : go_a3k<N, P, 1, false>(v, t, s);
 }
 
-template <int N, int P, int PFD>
+template <int N, int P, int PFD, int WT = 0>
 hipError_t go_b3k(const DevView& v, hipStream_t s) {
-    constexpr int W = b3_w(N);
+    if constexpr (WT == 0 && N >= 128 && N <= 1024) {
+        if (v.tile_w != inter_w(N)) return go_b3k<N, P, PFD, 4>(v, s);
+    }
+    constexpr int W = WT ? WT : b3_w(N);
     constexpr int T = W * N / kElems;
     const int items = v.units * (v.nx / W);
-    const int g = grid3(k_pass_b3<N, P, PFD>, T, items);
-    hipLaunchKernelGGL((k_pass_b3<N, P, PFD>), dim3(g), dim3(T), 0, s, v, items);
+    const int g = grid3(k_pass_b3<N, P, PFD, WT>, T, items);
+    hipLaunchKernelGGL((k_pass_b3<N, P, PFD, WT>), dim3(g), dim3(T), 0, s, v, items);
     return hipGetLastError();
 }
 
@@ -468,16 +474,19 @@ hipError_t go_b3(const DevView& v, hipStream_t s) {
     return go_b3k<N, P, 1>(v, s);
 }
 
-template <int N, bool NOSTORE = false, bool BAND = false, int PH = 2>
+template <int N, bool NOSTORE = false, bool BAND = false, int PH = 2, int WT = 0>
 hipError_t go_a4(const DevView& v, float t, hipStream_t s) {
+    if constexpr (WT == 0) {
+        if (v.tile_w != inter_w(N)) return go_a4<N, NOSTORE, BAND, PH, 4>(v, t, s);
+    }
     if constexpr (!BAND && !NOSTORE) {
-        if (v.nx != N) return go_a4<N, false, true, PH>(v, t, s);
+        if (v.nx != N) return go_a4<N, false, true, PH, WT>(v, t, s);
     }
     constexpr int T = N / 4;
     const int ipu = N / 2;
     const int items = v.units * ipu;
-    const int g = grid3(k_pass_a4<N, NOSTORE, BAND, PH>, T, items);
-    hipLaunchKernelGGL((k_pass_a4<N, NOSTORE, BAND, PH>), dim3(g), dim3(T), 0, s, v, t, ipu, items);
+    const int g = grid3(k_pass_a4<N, NOSTORE, BAND, PH, WT>, T, items);
+    hipLaunchKernelGGL((k_pass_a4<N, NOSTORE, BAND, PH, WT>), dim3(g), dim3(T), 0, s, v, t, ipu, items);
     return hipGetLastError();
 }
 

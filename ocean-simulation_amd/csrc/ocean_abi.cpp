@@ -62,6 +62,7 @@ struct ocean_ctx {
     int c4_bands = 0;        // OCEAN_C4_BANDS: N >= 2048 column passes per (unit, band); 0 = auto
     int chunk_min = 1 << 30; // OCEAN_CHUNK_MIN: units per chunk when one unit exceeds OCEAN_CHUNK_MIB
     int band_x0 = 0, band_nx = 0;  // column band of the fused passes (ocean_set_column_band); nx = n: whole
+    int tile_w = 8;                // column-tile width of the fused path's tile-major layouts (ocean_create)
     float4* waves = nullptr;
     float2* plane[4] = {nullptr, nullptr, nullptr, nullptr};
     float4* disp = nullptr;
@@ -113,7 +114,7 @@ struct ocean_ctx {
         v.tw = tw;
         v.casc = casc;
         v.gravity = params.gravity;
-        v.tile_w = ocean::fftcore::inter_w(n);
+        v.tile_w = tile_w;
         v.tplane = tplane;
         v.foam = foam;
         v.deriv_mips = deriv_mips;
@@ -260,6 +261,21 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
     if (const char* kc = std::getenv("OCEAN_CHUNK_MIB")) c->chunk_mib = std::atol(kc);
     if (const char* kb = std::getenv("OCEAN_C4_BANDS")) c->c4_bands = std::max(0, std::atoi(kb));
     if (const char* km = std::getenv("OCEAN_CHUNK_MIN")) c->chunk_min = std::max(1, std::atoi(km));
+    // Width of the fused path's column tiles.  With fewer tiles than CUs (one 512^2
+    // cascade: 32 tiles of 16 columns) pass B ran on an eighth of the chip, so small
+    // jobs take 4-column tiles.  OCEAN_TILE_W overrides (A/B).
+    c->tile_w = ocean::fftcore::inter_w(n);
+    {
+        int cus = 256;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
+            cus = 256;
+        const long tiles = (long)n_cascades * n_tiles * (n / c->tile_w);
+        if (n >= 128 && n <= 1024 && tiles < cus) c->tile_w = 4;
+        if (const char* kw = std::getenv("OCEAN_TILE_W")) {
+            const int w = std::atoi(kw);
+            if (n >= 128 && n <= 1024 && (w == 4 || w == ocean::fftcore::inter_w(n))) c->tile_w = w;
+        }
+    }
 
     auto alloc = [&](void** p, size_t bytes) -> bool {
         if (hipMalloc(p, bytes) != hipSuccess) return false;

@@ -36,7 +36,7 @@ struct DevView {
                           // T2[64] = exp(2 pi i 64 hi / N) (two-level table for N > 1024)
     const float* casc;    // [C][5] wavelength, cutoff_low, cutoff_high, swell, fade (device)
     float gravity;        // for the per-frame wave-data recompute (fused row pass)
-    int tile_w;           // width W = inter_w(N) of the tile-major layouts below
+    int tile_w;           // width W of the tile-major layouts below: inter_w(N), or 4 for small jobs
     float2* tplane;       // fused intermediate, P planes x [U][N/W][N][W] (tile-major), stride plane_stride
     float* foam;          // foam state, [U][N/W][N][W] (tile-major); TURB is its broadcast RGBA image
     float4* deriv_mips;   // OCEAN_F_MIPS: per slice, levels 1..log2 N concatenated (mip_chain texels)
@@ -81,7 +81,7 @@ hipError_t launch_mips(const DevView& v, hipStream_t s);
 // 16-wide tile-major intermediate) + C2 (with the pass-B epilogue); replace pass B.
 bool pass_c4_supported(int n);
 hipError_t launch_pass_c4(const DevView& v, hipStream_t s);
-// Mirror-pair row pass (N = 1024, 4 planes): one item = rows y and N - y; the
+// Mirror-pair row pass (N = 512 / 1024, 4 planes): one item = rows y and N - y; the
 // texels k and -k share wave data and the phase factor and read h0 once (h0k).
 bool pass_a4_supported(int n, int planes);
 hipError_t launch_pass_a_v4(const DevView& v, float t, hipStream_t s);

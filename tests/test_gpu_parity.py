@@ -206,6 +206,40 @@ def test_frames_vs_oracle(n, ncasc, flags):
     ctx.close()
 
 
+
+@pytest.mark.parametrize("n", [128, 1024])
+def test_five_cascades_vs_oracle(n):
+    """The ABI's maximum of 5 cascades (ocean.h; Water.shader:139) through the fused frame, a fifth
+    short-wave cascade added, against the oracle over 2 frames (foam included)."""
+    cas = O.SCENE_CASCADES + [dict(wavelength=9.0, cutoff_low=0.01, cutoff_high=50.0, swell=0.2, fade=0.05)]
+    ctx, (noise,) = make_ctx(n, cas)
+    oc = O.OracleOcean(n, O.scene_params(), cas, noise)
+    for t in (0.0, 2.5):
+        ctx.step(t)
+        disp, deriv, turb = oc.step(t)
+        assert_channels(ctx.read_all(oh.TEX_DISP)[..., :3], disp[..., :3], what=f"N={n} disp t={t}")
+        assert_channels(ctx.read_all(oh.TEX_DERIV), deriv, what=f"N={n} deriv t={t}")
+        assert_channels(ctx.read_all(oh.TEX_TURB), turb, what=f"N={n} turb t={t}")
+    ctx.close()
+
+
+@pytest.mark.parametrize("n,ncasc,wide", [(512, 3, "16"), (1024, 1, "8")])
+def test_narrow_column_tiles_bit_identical(n, ncasc, wide, monkeypatch):
+    """Jobs with fewer column tiles than CUs run the fused passes on 4-column tiles (ocean_create);
+    the frame equals the wide-tile frame bit for bit (OCEAN_TILE_W forces the wide layout)."""
+    cas = O.SCENE_CASCADES[:ncasc]
+    a, _ = make_ctx(n, cas)
+    monkeypatch.setenv("OCEAN_TILE_W", wide)
+    b, _ = make_ctx(n, cas)
+    for t in (0.5, 1.0):
+        a.step(t)
+        b.step(t)
+    for tex in (oh.TEX_DISP, oh.TEX_DERIV, oh.TEX_TURB):
+        np.testing.assert_array_equal(a.read_all(tex), b.read_all(tex))
+    a.close()
+    b.close()
+
+
 def test_fused_equals_unfused_to_rounding():
     n, cas = 256, O.SCENE_CASCADES
     a, _ = make_ctx(n, cas)
