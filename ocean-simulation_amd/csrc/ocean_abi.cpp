@@ -263,14 +263,15 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
     if (const char* km = std::getenv("OCEAN_CHUNK_MIN")) c->chunk_min = std::max(1, std::atoi(km));
     // Width of the fused path's column tiles.  With fewer tiles than CUs (one 512^2
     // cascade: 32 tiles of 16 columns) pass B ran on an eighth of the chip, so small
-    // jobs take 4-column tiles.  OCEAN_TILE_W overrides (A/B).
+    // jobs at N <= 512 take 4-column tiles (at N = 1024 pass A's
+    // 32-byte tile rows cost what pass B gains).  OCEAN_TILE_W overrides (A/B).
     c->tile_w = ocean::fftcore::inter_w(n);
     {
         int cus = 256;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
             cus = 256;
         const long tiles = (long)n_cascades * n_tiles * (n / c->tile_w);
-        if (n >= 128 && n <= 1024 && tiles < cus) c->tile_w = 4;
+        if (n >= 128 && n <= 512 && tiles < cus) c->tile_w = 4;
         if (const char* kw = std::getenv("OCEAN_TILE_W")) {
             const int w = std::atoi(kw);
             if (n >= 128 && n <= 1024 && (w == 4 || w == ocean::fftcore::inter_w(n))) c->tile_w = w;

@@ -223,11 +223,12 @@ def test_five_cascades_vs_oracle(n):
     ctx.close()
 
 
-@pytest.mark.parametrize("n,ncasc,wide", [(512, 3, "16"), (1024, 1, "8")])
+@pytest.mark.parametrize("n,ncasc,wide", [(256, 4, "32"), (512, 3, "16"), (1024, 1, "8")])
 def test_narrow_column_tiles_bit_identical(n, ncasc, wide, monkeypatch):
-    """Jobs with fewer column tiles than CUs run the fused passes on 4-column tiles (ocean_create);
-    the frame equals the wide-tile frame bit for bit (OCEAN_TILE_W forces the wide layout)."""
+    """Jobs at N <= 512 with fewer column tiles than CUs run the fused passes on 4-column tiles
+    (ocean_create); the frame equals the wide-tile frame bit for bit (OCEAN_TILE_W forces each)."""
     cas = O.SCENE_CASCADES[:ncasc]
+    monkeypatch.setenv("OCEAN_TILE_W", "4")
     a, _ = make_ctx(n, cas)
     monkeypatch.setenv("OCEAN_TILE_W", wide)
     b, _ = make_ctx(n, cas)
