@@ -9,7 +9,8 @@
 //   data (kx, 1/|k|, kz, omega) is recomputed from (x, y, cascade) with the init
 //   kernel's own arithmetic (spectrum_math.h wave_data, bit-identical) instead
 //   of being read: 16 B/texel less HBM traffic.  Outputs go to the tile-major
-//   intermediate [p][u][x/W][y][W], W = inter_w(N).
+//   intermediate [p][u][x/W][y][W], W = inter_w(N) (4 for small jobs at N <= 512,
+//   ocean_create).
 // Pass A4 (k_pass_a4, N = 512 / 1024 with 4 planes): the same per row pair
 //   (y, N - y), sharing wave data and exp(i omega t) between k and -k and
 //   reading h0 once through h0k (see the kernel).
@@ -68,9 +69,9 @@ __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems) void k_pass_a3(De
 #pragma unroll
         for (int r = 0; r < R0; ++r) hh[r] = bload4(w, (rr * N + j) * 16, r * NJ * 16);  // past-end rows read 0
     };
-    // N >= 2048: the 32-byte tile rows (W = 4) of 4 consecutive rows share each
-    // 128-B line of the intermediate; deal consecutive rows to one XCD (blockIdx b
-    // runs on XCD b % 8) so its L2 merges the partial lines before write-back
+    // N >= 2048: deal consecutive rows to one XCD (blockIdx b runs on XCD b % 8).
+    // Introduced for 4-wide tiles, whose 32-byte rows of 4 consecutive rows share a
+    // 128-B line that one L2 then merges; today's 16-wide tile rows are whole lines
     int item = (N >= 2048 && gridDim.x % 8 == 0) ? (int)(blockIdx.x % 8) * (int)(gridDim.x / 8) + (int)blockIdx.x / 8
                                                   : (int)blockIdx.x;
     if (item < items) load(item, h);
