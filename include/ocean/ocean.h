@@ -106,7 +106,9 @@ void ocean_destroy(ocean_ctx *ctx);
 
 /* Replaces the SetFloat/SetBuffer parameter bindings of
  * InitializeInitialSpectrumComputeShader (WaterBody.cs:130-148).
- * `cascades` has n_cascades entries.  Takes effect at the next ocean_init_spectrum. */
+ * `cascades` has n_cascades entries.  The values are only staged: they take effect
+ * at the next ocean_init_spectrum, and frames stepped before it keep running with
+ * the previous spectrum's constants (fused and unfused alike). */
 int ocean_set_params(ocean_ctx *ctx, const ocean_params *params, const ocean_cascade *cascades);
 
 /* Replaces GenerateRandomNoiseTexture + Texture2D.Apply (WaterBody.cs:86-100, :97):
@@ -129,9 +131,17 @@ int ocean_generate_noise(ocean_ctx *ctx, uint64_t seed);
 int ocean_generate_noise_device(ocean_ctx *ctx, uint64_t seed);
 
 /* Replaces CalculateInitialSpectrumTextures (WaterBody.cs:171-178):
- * InitialSpectrum.compute:99-129 then :135-143 for every tile and cascade.
- * Also zeroes the foam state (TURB).  Async on the ctx stream. */
+ * InitialSpectrum.compute:99-129 then :135-143 for every tile and cascade, with
+ * the parameters staged by ocean_set_params.  The foam state (TURB) is left as it
+ * is, as in the reference's re-init on a parameter change (the commented
+ * OnValidate, WaterBody.cs:324-337); it is zero after ocean_create.  Blocks until
+ * the staged constants are on the device, then runs async on the ctx stream. */
 int ocean_init_spectrum(ocean_ctx *ctx);
+
+/* Zeroes the foam accumulator (TURB, its mip chain and the internal foam state)
+ * of every tile and cascade, stream-ordered.  No reference counterpart: there the
+ * RenderTexture starts zeroed once (WaterBody.cs:229) and is never cleared. */
+int ocean_reset_foam(ocean_ctx *ctx);
 
 /* Replaces CalculateWavesTexturesAtTime(time) (WaterBody.cs:180-193, minus
  * GenerateMips): evolve -> 2D IFFT of every plane -> fill/foam for all tiles
@@ -174,7 +184,9 @@ int ocean_fill(ocean_ctx *ctx);
 int ocean_read(ocean_ctx *ctx, int texture, int tile, int cascade, void *dst, size_t bytes);
 
 /* Synchronous upload of one slice (foam state for resume, planes for
- * operator-level tests).  Same size rules as ocean_read. */
+ * operator-level tests).  Same size rules as ocean_read.  OCEAN_TEX_WAVES is
+ * writable only with OCEAN_F_UNFUSED (E_UNSUPPORTED otherwise): the fused row pass
+ * rebuilds the wave data from the active parameters every frame. */
 int ocean_write(ocean_ctx *ctx, int texture, int tile, int cascade, const void *src, size_t bytes);
 
 /* Zero-copy access for same-process consumers: base device pointer and total
@@ -191,7 +203,10 @@ int ocean_synchronize(ocean_ctx *ctx);
  * is bracketed by HIP events on the ctx stream; ocean_kernel_stats returns, for
  * kernel `kind` (0 = pass A / row pass, 1 = pass B / column pass, 2 = other),
  * the summed duration in ms and the launch count since the last reset
- * (synchronizes the stream). */
+ * (synchronizes the stream).  At most 2048 launches' events are held: past that
+ * the finished ones are folded into the sums (waiting for the oldest if none
+ * has finished), and disabling timing folds the rest, so a host that never
+ * polls holds a bounded number of events. */
 int ocean_set_kernel_timing(ocean_ctx *ctx, int enable);
 int ocean_kernel_stats(ocean_ctx *ctx, int kind, double *total_ms, long long *launches);
 

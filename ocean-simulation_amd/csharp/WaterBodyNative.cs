@@ -51,7 +51,8 @@ namespace OceanHip
             OceanNative.Check(OceanNative.ocean_set_params(ctx, ref p, cs), "ocean_set_params");
         }
 
-        // The commented OnValidate of WaterBody.cs:324-337: parameter change -> spectrum re-init.
+        // The commented OnValidate of WaterBody.cs:324-337: parameter change -> spectrum re-init
+        // (the foam accumulator carries over, as there).
         public void OnValidate()
         {
             if (ctx == IntPtr.Zero) return;
@@ -62,31 +63,45 @@ namespace OceanHip
         public void CalculateWavesTexturesAtTime(float time) =>
             OceanNative.Check(OceanNative.ocean_step(ctx, time), "ocean_step");
 
-        // WaterBody.Update (:284-297): step, then request the displacement slice 0
-        // asynchronously (AsyncGPUReadback.Request, :288-296); a completed request
-        // refreshes buoyancyData, as the reference's callback does.
-        IntPtr pending = IntPtr.Zero, pinned = IntPtr.Zero;
+        // WaterBody.Update (:284-297): step, then issue a new asynchronous request of the
+        // displacement slice 0 EVERY frame (AsyncGPUReadback.Request, :288); requests
+        // complete in order and each completed one refreshes buoyancyData, as the
+        // reference's callback does (:292-295).  Each request has its own pinned buffer.
+        const int MaxReadbacksInFlight = 8;  // the reference's request queue is engine-managed
+        readonly System.Collections.Generic.Queue<(IntPtr req, IntPtr buf)> readbacks =
+            new System.Collections.Generic.Queue<(IntPtr req, IntPtr buf)>();
+
+        void Complete((IntPtr req, IntPtr buf) r, bool wait)
+        {
+            int n = texturesSize * texturesSize * 4;
+            int st = wait ? (OceanNative.ocean_readback_wait(r.req) == OceanStatus.Ok ? 1 : -1)
+                          : OceanNative.ocean_readback_status(r.req);
+            if (st == 1)
+            {
+                buoyancyData ??= new float[n];
+                System.Runtime.InteropServices.Marshal.Copy(r.buf, buoyancyData, 0, n);
+            }                                              // st < 0: request.hasError, data dropped
+            OceanNative.ocean_readback_release(r.req);
+            OceanNative.ocean_host_free(r.buf);
+        }
 
         public void Update(float time)
         {
             CalculateWavesTexturesAtTime(time);
+            while (readbacks.Count > 0 && OceanNative.ocean_readback_status(readbacks.Peek().req) != 0)
+                Complete(readbacks.Dequeue(), false);
+            if (readbacks.Count >= MaxReadbacksInFlight) Complete(readbacks.Dequeue(), true);
             int n = texturesSize * texturesSize * 4;
-            if (pinned == IntPtr.Zero)
-                OceanNative.Check(OceanNative.ocean_host_alloc((UIntPtr)(n * sizeof(float)), out pinned), "ocean_host_alloc");
-            if (pending != IntPtr.Zero)
-            {
-                int st = OceanNative.ocean_readback_status(pending);
-                if (st == 0) return;                       // previous request still in flight
-                if (st == 1)
-                {
-                    buoyancyData ??= new float[n];
-                    System.Runtime.InteropServices.Marshal.Copy(pinned, buoyancyData, 0, n);
-                }
-                OceanNative.ocean_readback_release(pending); // st < 0: request.hasError, data dropped
-                pending = IntPtr.Zero;
-            }
-            OceanNative.Check(OceanNative.ocean_read_async(ctx, OceanTexture.Displacement, 0, 0, pinned,
-                                                           (UIntPtr)(n * sizeof(float)), out pending), "ocean_read_async");
+            OceanNative.Check(OceanNative.ocean_host_alloc((UIntPtr)(n * sizeof(float)), out var buf), "ocean_host_alloc");
+            var st = OceanNative.ocean_read_async(ctx, OceanTexture.Displacement, 0, 0, buf,
+                                                  (UIntPtr)(n * sizeof(float)), out var req);
+            if (st != OceanStatus.Ok) { OceanNative.ocean_host_free(buf); OceanNative.Check(st, "ocean_read_async"); }
+            readbacks.Enqueue((req, buf));
+        }
+
+        public void WaitForReadbacks()
+        {
+            while (readbacks.Count > 0) Complete(readbacks.Dequeue(), true);
         }
 
         // WaterBody.cs:195-209, including the mapping over [-texturesSize/2, texturesSize/2].
@@ -113,10 +128,12 @@ namespace OceanHip
 
         public void Dispose()
         {
-            if (pending != IntPtr.Zero) OceanNative.ocean_readback_release(pending);
-            pending = IntPtr.Zero;
-            if (pinned != IntPtr.Zero) OceanNative.ocean_host_free(pinned);
-            pinned = IntPtr.Zero;
+            while (readbacks.Count > 0)
+            {
+                var r = readbacks.Dequeue();
+                OceanNative.ocean_readback_release(r.req);
+                OceanNative.ocean_host_free(r.buf);
+            }
             if (ctx != IntPtr.Zero) OceanNative.ocean_destroy(ctx);
             ctx = IntPtr.Zero;
         }

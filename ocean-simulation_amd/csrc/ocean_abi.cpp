@@ -77,8 +77,12 @@ struct ocean_ctx {
     float4* turb_mips = nullptr;
     size_t mip_chain = 0;
     hipStream_t copy_stream = nullptr;  // ocean_read_async
-    // host state
+    // host state.  `params` and the device `casc` are what the kernels run with; set_params
+    // only stages new values, which ocean_init_spectrum makes active (ocean.h), so a
+    // frame stepped between the two still uses the spectrum's own constants.
     ocean::SpectrumParams params{};
+    ocean::SpectrumParams staged_params{};
+    float staged_casc[5 * ocean::kMaxCascades] = {};
     bool params_set = false;
     std::vector<bool> noise_set;
     bool spectrum_ready = false;
@@ -88,6 +92,7 @@ struct ocean_ctx {
     std::vector<TimedLaunch> pending;
     double kind_ms[3] = {0, 0, 0};
     long long kind_count[3] = {0, 0, 0};
+    static constexpr size_t kMaxPending = 2048;  // timed launches held before folding into kind_ms
 
     size_t texels() const { return (size_t)n * n; }
     size_t units() const { return (size_t)T * C; }
@@ -147,11 +152,41 @@ int enter(ocean_ctx* ctx) {
     return OCEAN_OK;
 }
 
-// Launch wrapper: brackets the launch with events when kernel timing is on.
+// Folds timed launches into kind_ms / kind_count and returns their events to the pool.
+// wait: synchronize the stream first (every pending launch is then finished); else fold
+// the finished prefix only (stream order: the first unfinished launch ends it).
+int fold_pending(ocean_ctx* ctx, bool wait) {
+    if (wait) OCEAN_HIP(hipStreamSynchronize(ctx->stream));
+    size_t k = 0;
+    for (; k < ctx->pending.size(); ++k) {
+        const TimedLaunch& t = ctx->pending[k];
+        if (!wait) {
+            const hipError_t q = hipEventQuery(t.b);
+            if (q == hipErrorNotReady) break;
+            if (q != hipSuccess) return hip_fail(q, "hipEventQuery");
+        }
+        float ms = 0.0f;
+        OCEAN_HIP(hipEventElapsedTime(&ms, t.a, t.b));
+        ctx->kind_ms[t.kind] += ms;
+        ctx->kind_count[t.kind] += 1;
+        ctx->event_pool.push_back(t.a);
+        ctx->event_pool.push_back(t.b);
+    }
+    ctx->pending.erase(ctx->pending.begin(), ctx->pending.begin() + k);
+    return OCEAN_OK;
+}
+
+// Launch wrapper: brackets the launch with events when kernel timing is on.  A host that
+// never polls ocean_kernel_stats holds at most kMaxPending launches' events.
 template <class F>
 int timed(ocean_ctx* ctx, int kind, F&& launch, const char* what) {
     hipEvent_t a = nullptr, b = nullptr;
     if (ctx->timing) {
+        if (ctx->pending.size() >= ocean_ctx::kMaxPending) {
+            if (int r = fold_pending(ctx, false)) return r;
+            if (ctx->pending.size() >= ocean_ctx::kMaxPending)
+                if (int r = fold_pending(ctx, true)) return r;
+        }
         a = ctx->take_event();
         b = ctx->take_event();
         if (!a || !b) return fail(OCEAN_E_DEVICE, "hipEventCreate failed");
@@ -374,9 +409,10 @@ int ocean_set_params(ocean_ctx* ctx, const ocean_params* params, const ocean_cas
         h[c * 5 + 3] = k.swell;
         h[c * 5 + 4] = k.fade;
     }
-    OCEAN_HIP(hipMemcpyAsync(ctx->casc, h, (size_t)ctx->C * 5 * 4, hipMemcpyHostToDevice, ctx->stream));
-    OCEAN_HIP(hipStreamSynchronize(ctx->stream));
-    ctx->params = {p.wind_speed, p.wind_dir_x, p.wind_dir_y, p.gravity, p.fetch, p.depth};
+    // staged only: the running spectrum (h0, and the wave data the fused row pass rebuilds
+    // every frame from casc + gravity) keeps its constants until ocean_init_spectrum
+    std::memcpy(ctx->staged_casc, h, sizeof(float) * 5 * ctx->C);
+    ctx->staged_params = {p.wind_speed, p.wind_dir_x, p.wind_dir_y, p.gravity, p.fetch, p.depth};
     ctx->params_set = true;
     return OCEAN_OK;
 }
@@ -416,15 +452,29 @@ int ocean_init_spectrum(ocean_ctx* ctx) {
     if (!ctx->params_set) return fail(OCEAN_E_STATE, "ocean_set_params must precede ocean_init_spectrum");
     for (int t = 0; t < ctx->T; ++t)
         if (!ctx->noise_set[t]) return fail(OCEAN_E_STATE, "noise not set for tile " + std::to_string(t));
+    // the staged parameters become active (stream-ordered: frames queued before this
+    // call still read the previous constants)
+    OCEAN_HIP(hipMemcpyAsync(ctx->casc, ctx->staged_casc, (size_t)ctx->C * 5 * 4, hipMemcpyHostToDevice, ctx->stream));
+    OCEAN_HIP(hipStreamSynchronize(ctx->stream));
+    ctx->params = ctx->staged_params;
     const ocean::DevView v = ctx->view();
     if (int r = timed(ctx, 2, [&] { return ocean::launch_init_spectrum(v, ctx->params, ctx->stream); },
                       "init_spectrum"))
         return r;
     if (int r = timed(ctx, 2, [&] { return ocean::launch_conjugate(v, ctx->stream); }, "conjugate")) return r;
-    if (ctx->turb) OCEAN_HIP(hipMemsetAsync(ctx->turb, 0, ctx->texels() * ctx->units() * 16, ctx->stream));
-    if (ctx->foam) OCEAN_HIP(hipMemsetAsync(ctx->foam, 0, ctx->texels() * ctx->units() * 4, ctx->stream));
+    // the foam state is left alone: the reference re-runs CalculateInitialSpectrumTextures on a
+    // parameter change (the commented OnValidate, WaterBody.cs:324-337) without touching
+    // _TurbulenceTextures; it starts at zero (ocean_create) and ocean_reset_foam clears it
     ctx->spectrum_ready = true;
     ctx->h0k_valid = ctx->h0k != nullptr;
+    return OCEAN_OK;
+}
+
+int ocean_reset_foam(ocean_ctx* ctx) {
+    if (int r = enter(ctx)) return r;
+    if (ctx->turb) OCEAN_HIP(hipMemsetAsync(ctx->turb, 0, ctx->texels() * ctx->units() * 16, ctx->stream));
+    if (ctx->foam) OCEAN_HIP(hipMemsetAsync(ctx->foam, 0, ctx->texels() * ctx->units() * 4, ctx->stream));
+    if (ctx->turb_mips) OCEAN_HIP(hipMemsetAsync(ctx->turb_mips, 0, ctx->mip_chain * ctx->units() * 16, ctx->stream));
     return OCEAN_OK;
 }
 
@@ -712,6 +762,10 @@ void ocean_host_free(void* p) {
 int ocean_write(ocean_ctx* ctx, int texture, int tile, int cascade, const void* src, size_t bytes) {
     if (int r = enter(ctx)) return r;
     if (!src) return fail(OCEAN_E_INVALID_ARG, "null source");
+    if (texture == OCEAN_TEX_WAVES && !(ctx->flags & OCEAN_F_UNFUSED))
+        return fail(OCEAN_E_UNSUPPORTED, "WAVES is read-only under the fused schedule (its row pass rebuilds the "
+                                         "wave data from the parameters every frame); create the context with "
+                                         "OCEAN_F_UNFUSED to drive ocean_step from uploaded wave data");
     char* dst = nullptr;
     if (int r = slice_ptr(ctx, texture, tile, cascade, bytes, &dst)) return r;
     OCEAN_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
@@ -774,6 +828,8 @@ int ocean_set_kernel_timing(ocean_ctx* ctx, int enable) {
             ctx->event_pool.push_back(e);
         }
     }
+    if (!enable && !ctx->pending.empty())  // launches timed so far still count at the next ocean_kernel_stats
+        if (int r = fold_pending(ctx, true)) return r;
     ctx->timing = enable != 0;
     return OCEAN_OK;
 }
@@ -806,16 +862,7 @@ int ocean_step_bytes(ocean_ctx* ctx, uint64_t* pass_a, uint64_t* pass_b) {
 int ocean_kernel_stats(ocean_ctx* ctx, int kind, double* total_ms, long long* launches) {
     if (int r = enter(ctx)) return r;
     if (kind < 0 || kind > 2 || !total_ms || !launches) return fail(OCEAN_E_INVALID_ARG, "bad kind or null output");
-    OCEAN_HIP(hipStreamSynchronize(ctx->stream));
-    for (auto& t : ctx->pending) {
-        float ms = 0.0f;
-        OCEAN_HIP(hipEventElapsedTime(&ms, t.a, t.b));
-        ctx->kind_ms[t.kind] += ms;
-        ctx->kind_count[t.kind] += 1;
-        ctx->event_pool.push_back(t.a);
-        ctx->event_pool.push_back(t.b);
-    }
-    ctx->pending.clear();
+    if (int r = fold_pending(ctx, true)) return r;
     *total_ms = ctx->kind_ms[kind];
     *launches = ctx->kind_count[kind];
     ctx->kind_ms[kind] = 0;

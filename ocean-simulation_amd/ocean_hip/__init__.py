@@ -61,6 +61,7 @@ EXPORTED_SYMBOLS = (
     "ocean_set_kernel_timing", "ocean_kernel_stats", "ocean_step_bytes", "ocean_read_mip", "ocean_get_mip_ptr",
     "ocean_generate_noise_device", "ocean_read_async", "ocean_readback_status", "ocean_readback_wait", "ocean_readback_release",
     "ocean_host_alloc", "ocean_host_free", "ocean_last_error", "ocean_abi_version", "ocean_set_column_band",
+    "ocean_reset_foam",
 )
 
 
@@ -101,6 +102,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "ocean_set_noise": ([P, i, P], i),
         "ocean_generate_noise": ([P, u64], i),
         "ocean_init_spectrum": ([P], i),
+        "ocean_reset_foam": ([P], i),
         "ocean_step": ([P, f], i),
         "ocean_evolve": ([P, f], i),
         "ocean_ifft2d": ([P, i], i),
@@ -195,6 +197,9 @@ class OceanContext:
 
     def init_spectrum(self) -> None:
         _check(self.lib.ocean_init_spectrum(self._h), "ocean_init_spectrum")
+
+    def reset_foam(self) -> None:
+        _check(self.lib.ocean_reset_foam(self._h), "ocean_reset_foam")
 
     def step(self, t: float) -> None:
         _check(self.lib.ocean_step(self._h, ctypes.c_float(t)), "ocean_step")
@@ -370,7 +375,7 @@ class WaterBody:
     def __post_init__(self):
         self.ctx: Optional[OceanContext] = None
         self.buoyancyData: Optional[np.ndarray] = None
-        self._readback: Optional[Readback] = None
+        self._readbacks: List[Readback] = []
 
     def params(self) -> dict:
         return dict(wind_speed=self.windSpeed, wind_dir_x=self.windDirection[0], wind_dir_y=self.windDirection[1],
@@ -392,29 +397,38 @@ class WaterBody:
         return self
 
     def OnValidate(self) -> None:
-        """Parameter change -> spectrum re-init (the commented OnValidate, WaterBody.cs:324-337)."""
+        """Parameter change -> spectrum re-init (the commented OnValidate, WaterBody.cs:324-337);
+        the foam accumulator carries over, as there."""
         self.ctx.set_params(self.params(), [c.as_dict() for c in self.cascades])
         self.ctx.init_spectrum()
 
     def CalculateWavesTexturesAtTime(self, time: float) -> None:
         self.ctx.step(time)
 
+    MAX_READBACKS_IN_FLIGHT = 8  # bound on queued requests (the reference's queue is engine-managed)
+
     def Update(self, time: float) -> None:
+        """WaterBody.Update (WaterBody.cs:284-297): step, then issue a new AsyncGPUReadback
+        request of displacement slice 0 EVERY frame (:288); requests complete in order and
+        each completed one refreshes buoyancyData, as the reference's callback does (:292-295)."""
         self.CalculateWavesTexturesAtTime(time)
-        rb = self._readback
-        if rb is not None:
-            if not rb.done():
-                return  # the previous request is still in flight
-            self.buoyancyData = rb.data
-            rb.release()
-        self._readback = self.ctx.read_async(TEX_DISP, 0, 0)
+        self._poll_readbacks()
+        if len(self._readbacks) >= self.MAX_READBACKS_IN_FLIGHT:
+            self._complete(self._readbacks.pop(0))
+        self._readbacks.append(self.ctx.read_async(TEX_DISP, 0, 0))
+
+    def _complete(self, rb: "Readback") -> None:
+        self.buoyancyData = rb.data
+        rb.release()
+
+    def _poll_readbacks(self) -> None:
+        while self._readbacks and self._readbacks[0].done():
+            self._complete(self._readbacks.pop(0))
 
     def WaitForReadback(self) -> None:
-        """Block until the pending readback (if any) has landed in buoyancyData."""
-        if self._readback is not None:
-            self.buoyancyData = self._readback.data
-            self._readback.release()
-            self._readback = None
+        """Block until every pending readback has landed (the last one in buoyancyData)."""
+        while self._readbacks:
+            self._complete(self._readbacks.pop(0))
 
     def GetWaterHeight(self, worldPosition) -> float:
         """WaterBody.cs:195-209, including its quirk of mapping world x,z over
@@ -442,9 +456,9 @@ class WaterBody:
         return self.ctx.read_all(TEX_TURB, tile)
 
     def OnDisable(self) -> None:
-        if self._readback is not None:
-            self._readback.release()
-            self._readback = None
+        for rb in self._readbacks:
+            rb.release()
+        self._readbacks = []
         if self.ctx is not None:
             self.ctx.close()
             self.ctx = None

@@ -185,26 +185,92 @@ def test_golden_fixtures(flags):
         ctx.close()
 
 
+def oracle_threads():
+    """Oracle threads for the full-size cases (the box's CPU share: OMP_NUM_THREADS there)."""
+    return int(os.environ.get("OMP_NUM_THREADS") or min(16, os.cpu_count() or 1))
+
+
 @pytest.mark.parametrize("n,ncasc,flags", [(256, 1, 0), (512, 1, oh.F_DISPLACEMENT_ONLY), (512, 3, 0),
                                            (1024, 4, 0), (1024, 4, oh.F_UNFUSED), (2048, 1, 0),
-                                           (4096, 1, 0), (4096, 1, oh.F_DISPLACEMENT_ONLY)])
+                                           (4096, 1, 0), (4096, 1, oh.F_DISPLACEMENT_ONLY), (4096, 4, 0)])
 def test_frames_vs_oracle(n, ncasc, flags):
     """BASELINE configs: cfg1-shaped 256^2 x1, cfg2 512^2 displacement only, the scene (512^2 x3),
-    cfg3 4 x 1024^2 full outputs, and one cfg5 cascade at 4096^2 (four-step column passes, the
-    radix-2 oracle at full size); 3 frames so the foam state is exercised."""
+    cfg3 4 x 1024^2 full outputs, one cfg5 cascade at 4096^2 and cfg5 whole (4 x 4096^2: a 2 GiB
+    plane array, 2^31 bytes) through the four-step column passes, against the radix-2 oracle at
+    full size; 3 frames (2 for cfg5 whole) so the foam state is exercised."""
     cas = O.SCENE_CASCADES[:ncasc]
     ctx, (noise,) = make_ctx(n, cas, flags=flags)
     nplanes = 2 if flags & oh.F_DISPLACEMENT_ONLY else 4
-    oc = O.OracleOcean(n, O.scene_params(), cas, noise, nplanes=nplanes)
-    for f, t in enumerate([0.0, 1.0 / 60.0, 100.0]):
-        ctx.step(t)
-        disp, deriv, turb = oc.step(t)
-        assert_channels(ctx.read_all(oh.TEX_DISP)[..., :3], disp[..., :3], what=f"disp f{f}")
-        if nplanes == 4:
-            assert_channels(ctx.read_all(oh.TEX_DERIV), deriv, what=f"deriv f{f}")
-            assert_channels(ctx.read_all(oh.TEX_TURB), turb, what=f"turb f{f}")
+    O.set_threads(oracle_threads() if n >= 2048 else 1)
+    try:
+        oc = O.OracleOcean(n, O.scene_params(), cas, noise, nplanes=nplanes)
+        times = [0.0, 1.0 / 60.0] if (n == 4096 and ncasc == 4) else [0.0, 1.0 / 60.0, 100.0]
+        for f, t in enumerate(times):
+            ctx.step(t)
+            disp, deriv, turb = oc.step(t)
+            assert_channels(ctx.read_all(oh.TEX_DISP)[..., :3], disp[..., :3], what=f"disp f{f}")
+            if nplanes == 4:
+                assert_channels(ctx.read_all(oh.TEX_DERIV), deriv, what=f"deriv f{f}")
+                assert_channels(ctx.read_all(oh.TEX_TURB), turb, what=f"turb f{f}")
+            del disp, deriv, turb
+    finally:
+        O.set_threads(1)
     ctx.close()
 
+
+@pytest.mark.parametrize("times", [(20000.0, 20000.0 + 1 / 60), (36000.0, 86400.0)])
+def test_large_time_vs_oracle(times):
+    """cfg3 (4 x 1024^2) at play times of 5.5 h to a day: the phase omega*t passes 2^17 rad
+    where sincos_fast hands over from its Cody-Waite path to the library sincosf
+    (spectrum_math.h), for the short cascade's high-omega band first (omega up to 14.9 rad/s
+    at L = 34, so past t = 8797 s; at 20000 s every texel with omega > 6.55 is past it).  The
+    reference computes the fp32 phase omega*t (TimeDependentSpectrum.compute:24-25); the oracle
+    runs the same fp32 product through the C library's sinf/cosf."""
+    n, cas = 1024, O.SCENE_CASCADES
+    ctx, (noise,) = make_ctx(n, cas)
+    oc = O.OracleOcean(n, O.scene_params(), cas, noise)
+    w = ctx.read_all(oh.TEX_WAVES)
+    assert float(w[..., 3].max()) * times[0] > 131072.0  # the hand-over is crossed
+    for t in times:
+        ctx.step(t)
+        disp, deriv, turb = oc.step(t)
+        assert_channels(ctx.read_all(oh.TEX_DISP)[..., :3], disp[..., :3], what=f"disp t={t}")
+        assert_channels(ctx.read_all(oh.TEX_DERIV), deriv, what=f"deriv t={t}")
+        assert_channels(ctx.read_all(oh.TEX_TURB), turb, what=f"turb t={t}")
+    ctx.close()
+
+
+def test_cfg4_shape_chunked_tiles():
+    """cfg4's per-GPU shard (32 tiles x 4 cascades x 512^2, 128 units) at the DEFAULT unit
+    chunking (192 MiB of intermediate = 24 units per chunk: boundaries at units 24, 48, ...,
+    which fall mid-ocean at tile 6, and a partial last chunk of 8 units): every tile equals a
+    single-tile context bit for bit, and two tiles match the oracle."""
+    n, cas, T, seed = 512, O.SCENE_CASCADES, 32, 20251121 + 32
+    ctx = oh.OceanContext(n, 4, T)
+    ctx.set_params(O.scene_params(), cas)
+    ctx.generate_noise(seed)
+    ctx.init_spectrum()
+    times = (0.25, 0.5)
+    for t in times:
+        ctx.step(t)
+    for tile in range(T):
+        single = oh.OceanContext(n, 4, 1)
+        single.set_params(O.scene_params(), cas)
+        single.generate_noise(seed + tile)
+        single.init_spectrum()
+        for t in times:
+            single.step(t)
+        for tex in (oh.TEX_DISP, oh.TEX_DERIV, oh.TEX_TURB):
+            np.testing.assert_array_equal(ctx.read_all(tex, tile), single.read_all(tex), err_msg=f"tile {tile}")
+        single.close()
+    for tile in (5, 31):
+        oc = O.OracleOcean(n, O.scene_params(), cas, ctx.read(oh.TEX_NOISE, tile))
+        for t in times:
+            disp, deriv, turb = oc.step(t)
+        assert_channels(ctx.read_all(oh.TEX_DISP, tile)[..., :3], disp[..., :3], what=f"tile {tile} disp")
+        assert_channels(ctx.read_all(oh.TEX_DERIV, tile), deriv, what=f"tile {tile} deriv")
+        assert_channels(ctx.read_all(oh.TEX_TURB, tile), turb, what=f"tile {tile} turb")
+    ctx.close()
 
 
 @pytest.mark.parametrize("n", [128, 1024])
@@ -271,18 +337,35 @@ def test_tiles_are_independent_oceans():
     ctx.close()
 
 
-def test_normals_derived_output():
+def normal_fp32(deriv):
+    """fp32 restatement of normal_from_deriv (spectrum_math.h; Water.shader:346-348 on one
+    cascade's derivatives) in the kernel's operation order: every step correctly rounded."""
+    d = deriv.astype(np.float32)
+    one = np.float32(1.0)
+    sx = d[..., 0] / (one + d[..., 2])
+    sz = d[..., 1] / (one + d[..., 3])
+    inv = one / np.sqrt((sx * sx + one) + sz * sz)
+    return np.stack([-sx * inv, inv, -sz * inv, np.zeros_like(inv)], -1)
+
+
+@pytest.mark.parametrize("flags", [0, oh.F_UNFUSED])
+def test_normals_derived_output(flags):
+    """NORMAL is normal_from_deriv applied to the context's own DERIV: bit-exact against the
+    fp32 restatement; DERIV itself is within 1e-5 of the oracle (as in every frame test), and
+    the normal within 1e-5 norm-relative per channel of an fp64 normal of the oracle's DERIV."""
     n, cas = 128, O.SCENE_CASCADES[:2]
-    ctx, (noise,) = make_ctx(n, cas, flags=oh.F_NORMALS)
+    ctx, (noise,) = make_ctx(n, cas, flags=flags | oh.F_NORMALS)
     ctx.step(0.5)
+    got_deriv = ctx.read_all(oh.TEX_DERIV)
+    got = ctx.read_all(oh.TEX_NORMAL)
+    np.testing.assert_array_equal(got, normal_fp32(got_deriv))
     _, deriv, _ = O.OracleOcean(n, O.scene_params(), cas, noise).step(0.5)
+    assert_channels(got_deriv, deriv, what="deriv")
     d = deriv.astype(np.float64)
     sx, sz = d[..., 0] / (1 + d[..., 2]), d[..., 1] / (1 + d[..., 3])
     nrm = np.stack([-sx, np.ones_like(sx), -sz], -1)
     nrm /= np.linalg.norm(nrm, axis=-1, keepdims=True)
-    got = ctx.read_all(oh.TEX_NORMAL)
-    assert np.abs(got[..., :3] - nrm).max() < 1e-4
-    assert np.all(got[..., 3] == 0)
+    assert_channels(got[..., :3], nrm, what="normal")
     ctx.close()
 
 
@@ -545,14 +628,15 @@ def test_chunked_frame_equals_whole_frame():
 
 
 # ------------------------------------------------- cascade subsets + column bands
-@pytest.mark.parametrize("n,ncasc,world", [(256, 2, 4), (512, 4, 8), (1024, 4, 8), (4096, 2, 4)])
+@pytest.mark.parametrize("n,ncasc,world", [(256, 2, 4), (512, 4, 8), (1024, 4, 8), (4096, 2, 4), (4096, 4, 8)])
 def test_split_ocean_shards_bit_identical(n, ncasc, world):
     """One ocean split over `world` GPUs by ocean_hip.shard.plan_shard (cascade blocks,
     then column bands: cfg5's 8-GPU split at world = 2 x cascades), each shard its own
     context here on one GPU: every texel of every shard equals the whole ocean's bit for
     bit (the same arithmetic per texel; no data exchange), and columns outside a shard's
     band stay untouched (zero).  N = 512 / 1024 run the mirror-pair row pass, 4096 the
-    four-step column passes."""
+    four-step column passes; (4096, 4, 8) is cfg5's real 8-GPU plan (one cascade, half the
+    columns per rank)."""
     from ocean_hip.shard import plan_shard
     cas = O.SCENE_CASCADES[:ncasc]
     whole, _ = make_ctx(n, cas)

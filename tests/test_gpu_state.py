@@ -1,0 +1,104 @@
+"""GPU tests of the boundary's state rules (include/ocean/ocean.h): staged parameters,
+foam carried over a re-init, WAVES writes under the fused schedule, bounded kernel-timing
+events.  The reference counterparts are WaterBody.cs's Awake / OnValidate / Update order
+(WaterBody.cs:211-256, :324-337, :284-297)."""
+import numpy as np
+import pytest
+
+import ocean_hip as oh
+import oracle as O
+
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("require_gpu")]
+
+WINDY = dict(O.scene_params(), wind_speed=14.0)
+
+
+def _ctx(n, cas, flags=0, params=None, seed=20251121):
+    ctx = oh.OceanContext(n, len(cas), 1, flags)
+    ctx.set_params(params or O.scene_params(), cas)
+    ctx.set_noise(0, O.generate_noise(n, seed))
+    ctx.init_spectrum()
+    return ctx
+
+
+@pytest.mark.parametrize("n", [256, 1024])
+def test_set_params_staged_until_init(n):
+    """ocean_set_params takes effect at the next ocean_init_spectrum: frames stepped in between
+    equal those of a context that never saw the new values (fused and unfused alike; the fused
+    row pass rebuilds wave data from the active constants every frame), and after the re-init
+    the frames equal a fresh context built with the new values (foam state aside)."""
+    cas = O.SCENE_CASCADES
+    changed = [dict(c, wavelength=c["wavelength"] * 0.5, cutoff_low=c["cutoff_low"] * 10) for c in cas]
+    for flags in (0, oh.F_UNFUSED):
+        a = _ctx(n, cas, flags)
+        b = _ctx(n, cas, flags)
+        a.set_params(WINDY, changed)
+        for t in (0.5, 1.0):
+            a.step(t)
+            b.step(t)
+        for tex in (oh.TEX_DISP, oh.TEX_DERIV, oh.TEX_TURB):
+            np.testing.assert_array_equal(a.read_all(tex), b.read_all(tex))
+        a.init_spectrum()
+        a.reset_foam()
+        fresh = oh.OceanContext(n, len(cas), 1, flags)
+        fresh.set_params(WINDY, changed)
+        fresh.set_noise(0, O.generate_noise(n, 20251121))
+        fresh.init_spectrum()
+        a.step(2.0)
+        fresh.step(2.0)
+        for tex in (oh.TEX_DISP, oh.TEX_DERIV, oh.TEX_TURB):
+            np.testing.assert_array_equal(a.read_all(tex), fresh.read_all(tex))
+        for c in (a, b, fresh):
+            c.close()
+
+
+def test_reinit_keeps_foam_and_reset_clears_it():
+    """Re-init on a parameter change keeps the foam accumulator (the reference's OnValidate
+    re-runs only CalculateInitialSpectrumTextures, WaterBody.cs:324-337); ocean_reset_foam
+    zeroes it, after which the next frame equals a fresh context's first frame."""
+    n, cas = 128, O.SCENE_CASCADES[:2]
+    a = _ctx(n, cas)
+    for t in (0.1, 0.2):
+        a.step(t)
+    before = a.read_all(oh.TEX_TURB)
+    assert before.max() > 0
+    a.set_params(WINDY, cas)
+    a.init_spectrum()
+    np.testing.assert_array_equal(a.read_all(oh.TEX_TURB), before)   # untouched by the re-init
+    a.step(0.3)
+    a.reset_foam()
+    assert not a.read_all(oh.TEX_TURB).any()
+    b = _ctx(n, cas, params=WINDY)
+    a.step(0.4)
+    b.step(0.4)
+    np.testing.assert_array_equal(a.read_all(oh.TEX_TURB), b.read_all(oh.TEX_TURB))
+    a.close()
+    b.close()
+
+
+def test_waves_write_only_unfused():
+    n, cas = 64, O.SCENE_CASCADES[:1]
+    f = _ctx(n, cas)
+    w = f.read(oh.TEX_WAVES)
+    with pytest.raises(oh.OceanError) as e:
+        f.write(oh.TEX_WAVES, w)
+    assert e.value.code == oh.E_UNSUPPORTED
+    u = _ctx(n, cas, oh.F_UNFUSED)
+    u.write(oh.TEX_WAVES, w * np.float32(1.0))  # allowed: the unfused evolve reads WAVES
+    f.close()
+    u.close()
+
+
+def test_kernel_timing_events_bounded():
+    """A host that enables timing and never polls: past 2048 held launches the finished ones
+    are folded into the sums; disabling timing folds the rest.  Every launch is counted."""
+    ctx = _ctx(32, O.SCENE_CASCADES[:1])
+    ctx.set_kernel_timing(True)
+    steps = 1500  # 3000 timed launches (pass A + pass B per step)
+    for f in range(steps):
+        ctx.step(f / 60.0)
+    ctx.set_kernel_timing(False)
+    ms_a, na = ctx.kernel_stats(0)
+    ms_b, nb = ctx.kernel_stats(1)
+    assert na == steps and nb == steps and ms_a > 0 and ms_b > 0
+    ctx.close()
