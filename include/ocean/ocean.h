@@ -230,6 +230,26 @@ int ocean_step_bytes(ocean_ctx *ctx, uint64_t *pass_a, uint64_t *pass_b);
 int ocean_read_mip(ocean_ctx *ctx, int texture, int tile, int cascade, int level, void *dst, size_t bytes);
 int ocean_get_mip_ptr(ocean_ctx *ctx, int texture, int level, void **ptr, size_t *slice_stride);
 
+/* Cascade-summed world sampling, the texture reads of the reference's consumer
+ * (Water.shader:314-348).  Point i of `points` is (world x,
+ * world z, lod) as float[3]; out[i] is float[12]:
+ *   out[12i + 0..3]  = sum_c DISP_c(uv_c).xyz, sum_c (1 - saturate(TURB_c(uv_c, lod).x))
+ *   out[12i + 4..7]  = sum_c DERIV_c(uv_c, lod)            (Dyx, Dyz, Dxx, Dzz)
+ *   out[12i + 8..11] = normalize(-sx, 1, -sz), 0 with s = (d.x / (1 + d.z), d.y / (1 + d.w))
+ * over the cascades c of tile `tile`, uv_c = (x, z) / L_c (L_c = the active cascade
+ * wavelength), summed in cascade order from 0.  Filtering (this library's definition;
+ * Unity's RenderTextures are Repeat-wrapped and trilinear, WaterBody.cs:112-113):
+ * on an m x m level, s = uv * m - 0.5, texels floor(s) and floor(s) + 1 mod m, weights
+ * f = s - floor(s), lerp(a, b, f) = a + f (b - a), x first then y.  DISP has no mips
+ * (WaterBody.cs:227) and is read at level 0; DERIV and TURB blend levels floor(lod)
+ * and floor(lod) + 1 (lod clamped to [0, log2 N]) when the context has OCEAN_F_MIPS,
+ * else level 0.  DISPLACEMENT_ONLY contexts return zero derivatives and turbulence.
+ * ocean_sample_world takes host buffers and blocks; ocean_sample_world_device takes
+ * device pointers (points 4-B aligned, out 16-B aligned) and is async on the ctx
+ * stream, ordered after the queued steps.  count = 0 is a no-op. */
+int ocean_sample_world(ocean_ctx *ctx, int tile, const float *points, int count, float *out);
+int ocean_sample_world_device(ocean_ctx *ctx, int tile, const float *points, int count, float *out);
+
 /* Asynchronous readback, the AsyncGPUReadback.Request(tex, 0, callback) of
  * WaterBody.cs:288-296: copies one slice (level 0) to `dst` on a copy stream once
  * the work queued so far on the ctx stream (e.g. the last ocean_step) has finished,

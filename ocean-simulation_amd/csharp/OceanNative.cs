@@ -99,6 +99,10 @@ namespace OceanHip
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
         public static extern OceanStatus ocean_get_mip_ptr(IntPtr ctx, OceanTexture tex, int level, out IntPtr ptr, out UIntPtr sliceStride);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
+        public static extern OceanStatus ocean_sample_world(IntPtr ctx, int tile, [In] float[] points, int count, [Out] float[] output);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
+        public static extern OceanStatus ocean_sample_world_device(IntPtr ctx, int tile, IntPtr points, int count, IntPtr output);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
         public static extern OceanStatus ocean_read_async(IntPtr ctx, OceanTexture tex, int tile, int cascade, IntPtr dst, UIntPtr bytes, out IntPtr request);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
         public static extern int ocean_readback_status(IntPtr request);   // 1 done, 0 pending, < 0 error (hasError)

@@ -116,6 +116,16 @@ namespace OceanHip
             return buoyancyData[(y * texturesSize + x) * 4 + 1];  // .g = Dy
         }
 
+        // What Water.shader reads at world positions (Water.shader:314-348): points are
+        // (x, z, lod) triples; per point 12 floats: summed displacement + turbulence,
+        // summed derivatives, normal (ocean.h ocean_sample_world).
+        public float[] SampleWorld(float[] points)
+        {
+            var output = new float[points.Length / 3 * 12];
+            OceanNative.Check(OceanNative.ocean_sample_world(ctx, 0, points, points.Length / 3, output), "ocean_sample_world");
+            return output;
+        }
+
         // Texture-out contract: device pointers for same-process renderers (WaterBody.cs:277-281).
         public IntPtr DeviceTexture(OceanTexture tex, out ulong bytes)
         {

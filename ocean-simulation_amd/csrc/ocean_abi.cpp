@@ -803,6 +803,43 @@ int ocean_synchronize(ocean_ctx* ctx) {
     return OCEAN_OK;
 }
 
+static int check_sample(ocean_ctx* ctx, int tile, const float* pts, int count, float* out) {
+    if (int r = enter(ctx)) return r;
+    if (tile < 0 || tile >= ctx->T) return fail(OCEAN_E_INVALID_ARG, "tile out of range");
+    if (count < 0) return fail(OCEAN_E_INVALID_ARG, "negative point count");
+    if (count > 0 && (!pts || !out)) return fail(OCEAN_E_INVALID_ARG, "null points or output");
+    return OCEAN_OK;
+}
+
+int ocean_sample_world_device(ocean_ctx* ctx, int tile, const float* points, int count, float* out) {
+    if (int r = check_sample(ctx, tile, points, count, out)) return r;
+    const ocean::DevView v = ctx->view();
+    return timed(ctx, 2, [&] { return ocean::launch_sample_world(v, tile, points, count, out, ctx->stream); },
+                 "sample_world");
+}
+
+int ocean_sample_world(ocean_ctx* ctx, int tile, const float* points, int count, float* out) {
+    if (int r = check_sample(ctx, tile, points, count, out)) return r;
+    if (count == 0) return OCEAN_OK;
+    const size_t in_bytes = (size_t)count * 3 * 4, out_bytes = (size_t)count * 12 * 4;
+    const size_t out_off = (in_bytes + 255) & ~(size_t)255;  // float4 output rows stay 16-B aligned
+    void* d = nullptr;
+    OCEAN_HIP(hipMallocAsync(&d, out_off + out_bytes, ctx->stream));
+    float* d_in = static_cast<float*>(d);
+    float* d_out = reinterpret_cast<float*>(static_cast<char*>(d) + out_off);
+    hipError_t e = hipMemcpyAsync(d_in, points, in_bytes, hipMemcpyHostToDevice, ctx->stream);
+    int r = OCEAN_OK;
+    if (e == hipSuccess) r = ocean_sample_world_device(ctx, tile, d_in, count, d_out);
+    if (e == hipSuccess && r == OCEAN_OK) e = hipMemcpyAsync(out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream);
+    const hipError_t ef = hipFreeAsync(d, ctx->stream);
+    const hipError_t es = hipStreamSynchronize(ctx->stream);
+    if (r != OCEAN_OK) return r;
+    if (e != hipSuccess) return hip_fail(e, "ocean_sample_world copy");
+    if (ef != hipSuccess) return hip_fail(ef, "hipFreeAsync");
+    if (es != hipSuccess) return hip_fail(es, "hipStreamSynchronize");
+    return OCEAN_OK;
+}
+
 int ocean_set_column_band(ocean_ctx* ctx, int x_begin, int x_count) {
     if (int r = enter(ctx)) return r;
     const int n = ctx->n;

@@ -76,6 +76,8 @@ hipError_t launch_pass_a_v3(const DevView& v, float t, hipStream_t s);
 hipError_t launch_pass_b_v3(const DevView& v, hipStream_t s);
 // mips.hip: box-filter mip chains of DERIV and TURB (OCEAN_F_MIPS)
 hipError_t launch_mips(const DevView& v, hipStream_t s);
+// sample.hip: cascade-summed world sampling (Water.shader:314-348), device pointers
+hipError_t launch_sample_world(const DevView& v, int tile, const float* pts, int count, float* out, hipStream_t s);
 
 // fft4k.hip (N = 2048, 4096): four-step column passes C1 (in place on the
 // 16-wide tile-major intermediate) + C2 (with the pass-B epilogue); replace pass B.

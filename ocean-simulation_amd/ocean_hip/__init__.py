@@ -61,7 +61,7 @@ EXPORTED_SYMBOLS = (
     "ocean_set_kernel_timing", "ocean_kernel_stats", "ocean_step_bytes", "ocean_read_mip", "ocean_get_mip_ptr",
     "ocean_generate_noise_device", "ocean_read_async", "ocean_readback_status", "ocean_readback_wait", "ocean_readback_release",
     "ocean_host_alloc", "ocean_host_free", "ocean_last_error", "ocean_abi_version", "ocean_set_column_band",
-    "ocean_reset_foam",
+    "ocean_reset_foam", "ocean_sample_world", "ocean_sample_world_device",
 )
 
 
@@ -103,6 +103,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "ocean_generate_noise": ([P, u64], i),
         "ocean_init_spectrum": ([P], i),
         "ocean_reset_foam": ([P], i),
+        "ocean_sample_world": ([P, i, P, i, P], i),
+        "ocean_sample_world_device": ([P, i, P, i, P], i),
         "ocean_step": ([P, f], i),
         "ocean_evolve": ([P, f], i),
         "ocean_ifft2d": ([P, i], i),
@@ -243,6 +245,18 @@ class OceanContext:
         p, st = ctypes.c_void_p(), ctypes.c_size_t()
         _check(self.lib.ocean_get_mip_ptr(self._h, tex, level, ctypes.byref(p), ctypes.byref(st)), "ocean_get_mip_ptr")
         return p.value, st.value
+
+    def sample_world(self, points: np.ndarray, tile: int = 0) -> np.ndarray:
+        """Cascade-summed world sampling (Water.shader:314-348; ocean.h ocean_sample_world):
+        points float[M][3] = (world x, world z, lod) -> float32[M][3][4]: (Dx, Dy, Dz,
+        turbulence), (Dyx, Dyz, Dxx, Dzz), (normal x, y, z, 0)."""
+        p = np.ascontiguousarray(points, np.float32)
+        if p.ndim != 2 or p.shape[1] != 3:
+            raise ValueError(f"points must be float32[M][3], got {p.shape}")
+        out = np.empty((p.shape[0], 3, 4), np.float32)
+        _check(self.lib.ocean_sample_world(self._h, tile, p.ctypes.data, p.shape[0], out.ctypes.data),
+               "ocean_sample_world")
+        return out
 
     def read_async(self, tex: int, tile: int = 0, cascade: int = 0) -> "Readback":
         """AsyncGPUReadback.Request (WaterBody.cs:288-296): copy one slice into pinned
@@ -444,6 +458,11 @@ class WaterBody:
         x = min(max(int(u * n), 0), n - 1)
         y = min(max(int(v * n), 0), n - 1)
         return float(self.buoyancyData[y, x, 1])
+
+    def SampleWorld(self, points, tile: int = 0) -> np.ndarray:
+        """What Water.shader reads at world positions (x, z, lod): summed displacement,
+        derivatives, turbulence and the normal (Water.shader:314-348)."""
+        return self.ctx.sample_world(np.asarray(points, np.float32).reshape(-1, 3), tile)
 
     # texture-out contract (material properties, WaterBody.cs:277-281)
     def DisplacementsTextures(self, tile: int = 0) -> np.ndarray:

@@ -293,6 +293,89 @@ class ref64:
         return disp, deriv, foam
 
 
+# ------------------------------------------------------------ world sampling
+def _bil(u, v, m):
+    """Bilinear tap coordinates on an m x m level (ocean.h ocean_sample_world), fp32."""
+    f32 = np.float32
+    fm = f32(m)
+    inv = f32(1.0) / fm
+    sx = u * fm - f32(0.5)
+    sy = v * fm - f32(0.5)
+    flx, fly = np.floor(sx), np.floor(sy)
+    ix = (flx - fm * np.floor(flx * inv)).astype(np.int64)
+    iy = (fly - fm * np.floor(fly * inv)).astype(np.int64)
+    return ix, (ix + 1) & (m - 1), iy, (iy + 1) & (m - 1), sx - flx, sy - fly
+
+
+def _lerp(a, b, f):
+    return a + f[..., None] * (b - a)
+
+
+def _tap(tex, u, v):
+    """tex [m][m][4] float32, u/v float32[M] -> [M][4] (Repeat wrap, x then y)."""
+    m = tex.shape[0]
+    x0, x1, y0, y1, fx, fy = _bil(u, v, m)
+    return _lerp(_lerp(tex[y0, x0], tex[y0, x1], fx), _lerp(tex[y1, x0], tex[y1, x1], fx), fy)
+
+
+def _tri(levels, u, v, lod):
+    """levels[0..log2 N] of one slice; lod float32[M] (None: level 0 only)."""
+    if lod is None or len(levels) == 1:
+        return _tap(levels[0], u, v)
+    logn = len(levels) - 1
+    out = _tap(levels[0], u, v)
+    pos = lod > 0
+    if pos.any():
+        lc = np.minimum(lod[pos], np.float32(logn))
+        l0 = np.floor(lc).astype(np.int64)
+        l1 = np.minimum(l0 + 1, logn)
+        f = lc - l0.astype(np.float32)
+        a = np.empty((pos.sum(), 4), np.float32)
+        b = np.empty_like(a)
+        for lv in range(logn + 1):
+            s0, s1 = l0 == lv, l1 == lv
+            if s0.any():
+                a[s0] = _tap(levels[lv], u[pos][s0], v[pos][s0])
+            if s1.any():
+                b[s1] = _tap(levels[lv], u[pos][s1], v[pos][s1])
+        out[pos] = _lerp(a, b, f)
+    return out
+
+
+def sample_world(disp, deriv, turb, lengths, points, deriv_mips=None, turb_mips=None):
+    """fp32 restatement of ocean_sample_world (Water.shader:314-348 with the library's stated
+    filtering, include/ocean/ocean.h): disp/deriv/turb [C][N][N][4] of one tile (deriv/turb
+    None for displacement-only), lengths [C], points [M][3] = (x, z, lod), optional mip
+    chains as lists per cascade of levels 1..log2 N -> [M][3][4]."""
+    f32 = np.float32
+    pts = np.asarray(points, f32)
+    x, z, lod = pts[:, 0], pts[:, 1], pts[:, 2]
+    M = pts.shape[0]
+    d_sum = np.zeros((M, 4), f32)
+    g_sum = np.zeros((M, 4), f32)
+    t_sum = np.zeros(M, f32)
+    for c, L in enumerate(lengths):
+        L = f32(L)
+        u, v = x / L, z / L
+        d_sum = d_sum + _tap(disp[c].astype(f32), u, v)
+        if deriv is not None:
+            dl = [deriv[c]] + (list(deriv_mips[c]) if deriv_mips is not None else [])
+            tl = [turb[c]] + (list(turb_mips[c]) if turb_mips is not None else [])
+            g_sum = g_sum + _tri(dl, u, v, lod if deriv_mips is not None else None)
+            tb = _tri(tl, u, v, lod if turb_mips is not None else None)[:, 0]
+            t_sum = t_sum + (f32(1.0) - np.minimum(np.maximum(tb, f32(0.0)), f32(1.0)))
+    one = f32(1.0)
+    sx = g_sum[:, 0] / (one + g_sum[:, 2])
+    sz = g_sum[:, 1] / (one + g_sum[:, 3])
+    inv = one / np.sqrt((sx * sx + one) + sz * sz)
+    out = np.empty((M, 3, 4), f32)
+    out[:, 0, :3] = d_sum[:, :3]
+    out[:, 0, 3] = t_sum
+    out[:, 1] = g_sum
+    out[:, 2] = np.stack([-sx * inv, inv, -sz * inv, np.zeros_like(inv)], -1)
+    return out
+
+
 def scene_params(shallow: bool = False) -> dict:
     """WaterBody values from Assets/Scenes/Waves.unity:1305-1310 (depth 4 = script default, WaterBody.cs:14)."""
     return dict(wind_speed=8.0, wind_dir_x=1.0, wind_dir_y=-1.0, gravity=9.81, fetch=50000.0,

@@ -246,3 +246,28 @@ def test_threaded_oracle_frames_identical():
                 np.testing.assert_array_equal(x, y)
     finally:
         O.set_threads(1)
+
+
+def test_sample_world_restatement_known_answers():
+    """oracle.sample_world (the checker of ocean_sample_world): texel centres return the texel,
+    Repeat wrap, summing over cascades, lod blending of two constant levels, and the normal of a
+    flat sea (0, 1, 0)."""
+    n, L = 16, 32.0
+    rng = np.random.default_rng(0)
+    disp = rng.standard_normal((2, n, n, 4)).astype(np.float32)
+    deriv = np.zeros((2, n, n, 4), np.float32)
+    turb = np.full((2, n, n, 4), 0.25, np.float32)
+    pts = np.array([[(3 + 0.5) * L / n, (5 + 0.5) * L / n, 0.0],
+                    [(3 + 0.5) * L / n + L, (5 + 0.5) * L / n - 3 * L, 0.0]], np.float32)
+    out = O.sample_world(disp[:1], deriv[:1], turb[:1], [L], pts)
+    np.testing.assert_allclose(out[0, 0, :3], disp[0, 5, 3, :3], atol=1e-6)
+    np.testing.assert_allclose(out[1], out[0], atol=1e-5)
+    assert out[0, 0, 3] == np.float32(0.75)
+    np.testing.assert_array_equal(out[0, 2], [-0.0, 1.0, -0.0, 0.0])
+    two = O.sample_world(disp, deriv, turb, [L, L], pts[:1])
+    np.testing.assert_allclose(two[0, 0, :3], disp[0, 5, 3, :3] + disp[1, 5, 3, :3], atol=1e-6)
+    # lod 1.25 between a level-1 value of 1 and a level-2 value of 5 -> 1 + 0.25 * 4 = 2
+    levels = [[np.full((n >> k, n >> k, 4), float(v), np.float32) for k, v in ((1, 1.0), (2, 5.0), (3, 0.0), (4, 0.0))]]
+    p = np.array([[1.0, 2.0, 1.25]], np.float32)
+    o = O.sample_world(disp[:1], deriv[:1], turb[:1], [L], p, deriv_mips=levels, turb_mips=levels)
+    np.testing.assert_allclose(o[0, 1], [2.0] * 4, atol=1e-6)
