@@ -3,7 +3,7 @@
 # Usage: tools/pmc_sq.sh "<env,env> <env>..."; output gpurun_out/sq_<i>/
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
-ARGS="--steps 50 --warmup 5 --no-cpu-baseline --no-ifft-stage"
+ARGS=${ARGS:-"--steps 50 --warmup 5 --no-cpu-baseline --no-ifft-stage --no-beyond-cache"}
 i=0
 for cfg in $1; do
   i=$((i+1)); OUT=gpurun_out/sq_$i; mkdir -p $OUT; echo "$cfg" > $OUT/cfg
