@@ -6,7 +6,7 @@
 # Usage: tools/profile.sh <tag> [bench args...]
 set -o pipefail
 TAG=${1:-r01}; shift
-ARGS=${@:---steps 200 --warmup 20 --no-cpu-baseline --no-ifft-stage}
+ARGS=${@:---steps 200 --warmup 20 --no-cpu-baseline --no-ifft-stage --no-beyond-cache}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
