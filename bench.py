@@ -278,10 +278,11 @@ def main():
     barrier()
     elapsed = t1 - t0
 
-    # kernel region: the same K frames again with HIP events around every launch
-    # on the ctx stream (ocean_set_kernel_timing) -> per-kernel average durations
-    # for the roofline.  Kept out of the timed region: an event pair per launch
-    # adds ~2 us of gap per kernel on this stack.
+    # kernel region: the same K frames again with HIP events attached to every kernel
+    # dispatch on the ctx stream (ocean_set_kernel_timing; hipExtLaunchKernel start/stop
+    # events, so the durations are the kernels' own and agree with rocprofv3 --stats) ->
+    # per-kernel average durations for the roofline.  Kept out of the timed region: the
+    # event bookkeeping still lengthens a step by ~10 %.
     ctx.set_kernel_timing(True)
     ctx.kernel_stats(0), ctx.kernel_stats(1), ctx.kernel_stats(2)  # reset
     ctx.synchronize()

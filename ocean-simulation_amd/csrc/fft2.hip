@@ -155,7 +155,7 @@ struct Rows2 {
         const int total = np * v->units * N;
         const int items = (total + B - 1) / B;
         const int g = persistent_grid(k_rows2<N, B>, T, items);
-        hipLaunchKernelGGL((k_rows2<N, B>), dim3(g), dim3(T), 0, s, v->plane[p], total, v->tw);
+        launch((k_rows2<N, B>), dim3(g), dim3(T), 0, s, v->plane[p], total, v->tw);
         return hipGetLastError();
     }
     static hipError_t go(const DevView* v, int p, int np, hipStream_t s) {
@@ -169,7 +169,7 @@ struct Cols2 {
         constexpr int T = W * N / kElems;
         const int items = np * v->units * (N / W);
         const int g = persistent_grid(k_cols2<N>, T, items);
-        hipLaunchKernelGGL(k_cols2<N>, dim3(g), dim3(T), 0, s, v->plane[p], items, v->tw);
+        launch(k_cols2<N>, dim3(g), dim3(T), 0, s, v->plane[p], items, v->tw);
         return hipGetLastError();
     }
 };

@@ -440,7 +440,7 @@ hipError_t go_a3k(const DevView& v, float t, hipStream_t s) {
     const int total = v.units * N;
     const int items = (total + RB - 1) / RB;
     const int g = grid3(k_pass_a3<N, P, RS, PF, NOSTORE, BAND, WT>, T, items);
-    hipLaunchKernelGGL((k_pass_a3<N, P, RS, PF, NOSTORE, BAND, WT>), dim3(g), dim3(T), 0, s, v, t, total);
+    launch((k_pass_a3<N, P, RS, PF, NOSTORE, BAND, WT>), dim3(g), dim3(T), 0, s, v, t, total);
     return hipGetLastError();
 }
 
@@ -464,7 +464,7 @@ hipError_t go_b3k(const DevView& v, hipStream_t s) {
     constexpr int T = W * N / kElems;
     const int items = v.units * (v.nx / W);
     const int g = grid3(k_pass_b3<N, P, PFD, WT>, T, items);
-    hipLaunchKernelGGL((k_pass_b3<N, P, PFD, WT>), dim3(g), dim3(T), 0, s, v, items);
+    launch((k_pass_b3<N, P, PFD, WT>), dim3(g), dim3(T), 0, s, v, items);
     return hipGetLastError();
 }
 
@@ -487,7 +487,7 @@ hipError_t go_a4(const DevView& v, float t, hipStream_t s) {
     const int ipu = N / 2;
     const int items = v.units * ipu;
     const int g = grid3(k_pass_a4<N, NOSTORE, BAND, PH, WT>, T, items);
-    hipLaunchKernelGGL((k_pass_a4<N, NOSTORE, BAND, PH, WT>), dim3(g), dim3(T), 0, s, v, t, ipu, items);
+    launch((k_pass_a4<N, NOSTORE, BAND, PH, WT>), dim3(g), dim3(T), 0, s, v, t, ipu, items);
     return hipGetLastError();
 }
 

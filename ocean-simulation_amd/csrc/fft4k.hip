@@ -212,7 +212,7 @@ hipError_t go_c1(const DevView& v, hipStream_t s) {
     // two workgroups per CU, not the four that fit: cfg5 column passes 1.72 -> 1.67 ms
     // (three per CU: 1.70 ms), DESIGN.md section 3
     const int g = grid4(k_col4s1<N>, T, items, 2);
-    hipLaunchKernelGGL((k_col4s1<N>), dim3(g), dim3(T), 0, s, v, items);
+    launch((k_col4s1<N>), dim3(g), dim3(T), 0, s, v, items);
     return hipGetLastError();
 }
 
@@ -221,7 +221,7 @@ hipError_t go_c2(const DevView& v, hipStream_t s) {
     constexpr int T = kSeq * kL1 / kElems;
     const int items = v.units * (v.nx / kWT) * ((N / kL1) / (kSeq / kWT));
     const int g = grid4(k_col4s2<N, P>, T, items);
-    hipLaunchKernelGGL((k_col4s2<N, P>), dim3(g), dim3(T), 0, s, v, items);
+    launch((k_col4s2<N, P>), dim3(g), dim3(T), 0, s, v, items);
     return hipGetLastError();
 }
 

@@ -89,10 +89,10 @@ hipError_t launch_mips(const DevView& v, hipStream_t s) {
     int levels = 0;
     while ((1 << levels) < blk) ++levels;  // levels 1..log2(blk) from the block kernel
     const int bps = (n / blk) * (n / blk);
-    hipLaunchKernelGGL(k_mips_block, dim3(bps, v.units, 2), dim3(256), 0, s, v, blk, levels);
+    launch(k_mips_block, dim3(bps, v.units, 2), dim3(256), 0, s, v, blk, levels);
     if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
     if (blk < n) {
-        hipLaunchKernelGGL(k_mips_tail, dim3(v.units, 2), dim3(256), 0, s, v, levels + 1);
+        launch(k_mips_tail, dim3(v.units, 2), dim3(256), 0, s, v, levels + 1);
         return hipGetLastError();
     }
     return hipSuccess;

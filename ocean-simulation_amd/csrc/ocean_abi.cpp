@@ -41,6 +41,13 @@ struct TimedLaunch {
 
 }  // namespace
 
+namespace ocean {
+LaunchEvents*& launch_events() {
+    thread_local LaunchEvents* slot = nullptr;
+    return slot;
+}
+}  // namespace ocean
+
 // Host noise generator (WaterBody.cs:71-100 with this library's documented
 // uniform source).  Defined in noise.cpp.
 namespace ocean {
@@ -176,28 +183,31 @@ int fold_pending(ocean_ctx* ctx, bool wait) {
     return OCEAN_OK;
 }
 
-// Launch wrapper: brackets the launch with events when kernel timing is on.  A host that
-// never polls ocean_kernel_stats holds at most kMaxPending launches' events.
+// Launch wrapper: when kernel timing is on, the kernels launched by `launch` carry an event
+// pair (ocean_internal.h, launch_events).  A host that never polls ocean_kernel_stats holds
+// at most kMaxPending launches' events.
 template <class F>
 int timed(ocean_ctx* ctx, int kind, F&& launch, const char* what) {
-    hipEvent_t a = nullptr, b = nullptr;
-    if (ctx->timing) {
-        if (ctx->pending.size() >= ocean_ctx::kMaxPending) {
-            if (int r = fold_pending(ctx, false)) return r;
-            if (ctx->pending.size() >= ocean_ctx::kMaxPending)
-                if (int r = fold_pending(ctx, true)) return r;
-        }
-        a = ctx->take_event();
-        b = ctx->take_event();
-        if (!a || !b) return fail(OCEAN_E_DEVICE, "hipEventCreate failed");
-        OCEAN_HIP(hipEventRecord(a, ctx->stream));
+    if (!ctx->timing) {
+        const hipError_t e = launch();
+        return e == hipSuccess ? OCEAN_OK : hip_fail(e, what);
     }
-    hipError_t e = launch();
+    if (ctx->pending.size() >= ocean_ctx::kMaxPending) {
+        if (int r = fold_pending(ctx, false)) return r;
+        if (ctx->pending.size() >= ocean_ctx::kMaxPending)
+            if (int r = fold_pending(ctx, true)) return r;
+    }
+    ocean::LaunchEvents ev{ctx->take_event(), ctx->take_event(), false};
+    if (!ev.start || !ev.stop) return fail(OCEAN_E_DEVICE, "hipEventCreate failed");
+    ocean::launch_events() = &ev;  // the kernels of this entry carry the events (ocean_internal.h)
+    const hipError_t e = launch();
+    ocean::launch_events() = nullptr;
     if (e != hipSuccess) return hip_fail(e, what);
-    if (ctx->timing) {
-        OCEAN_HIP(hipEventRecord(b, ctx->stream));
-        ctx->pending.push_back({kind, a, b});
+    if (!ev.launched) {  // nothing was launched: an empty interval
+        OCEAN_HIP(hipEventRecord(ev.start, ctx->stream));
+        OCEAN_HIP(hipEventRecord(ev.stop, ctx->stream));
     }
+    ctx->pending.push_back({kind, ev.start, ev.stop});
     return OCEAN_OK;
 }
 

@@ -2,12 +2,32 @@
 // kernel translation units (spectrum.hip, fft2/3/4k.hip, mips.hip).  Not part of the ABI.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "ocean/ocean.h"
 
 namespace ocean {
+
+// Kernel timing (ocean_set_kernel_timing): the C-ABI layer points this thread's slot at an
+// event pair around one entry point's launches; every kernel launch goes through launch(),
+// which attaches the pair to the dispatch itself (hipExtLaunchKernel: start of the first
+// kernel, end of the last), so the measured time is the kernels' own, as rocprofv3 reports it,
+// with no marker packets between them.
+struct LaunchEvents {
+    hipEvent_t start, stop;
+    bool launched;
+};
+LaunchEvents*& launch_events();  // thread-local slot, ocean_abi.cpp
+
+template <class F, class... Args>
+inline void launch(F kernel, dim3 grid, dim3 block, uint32_t shmem, hipStream_t s, Args... args) {
+    LaunchEvents* e = launch_events();
+    hipExtLaunchKernelGGL(kernel, grid, block, shmem, s, e && !e->launched ? e->start : nullptr,
+                          e ? e->stop : nullptr, 0, args...);
+    if (e) e->launched = true;
+}
 
 constexpr int kMaxCascades = 5;  // the consumer shader caps cascades at 5 (Water.shader:139)
 

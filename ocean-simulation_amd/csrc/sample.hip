@@ -112,7 +112,7 @@ __global__ __launch_bounds__(256) void k_sample_world(DevView v, int tile, const
 hipError_t launch_sample_world(const DevView& v, int tile, const float* pts, int count, float* out, hipStream_t s) {
     if (count <= 0) return hipSuccess;
     const unsigned g = (unsigned)((count + 255) / 256);
-    hipLaunchKernelGGL(k_sample_world, dim3(g), dim3(256), 0, s, v, tile, pts, count, reinterpret_cast<float4*>(out));
+    launch(k_sample_world, dim3(g), dim3(256), 0, s, v, tile, pts, count, reinterpret_cast<float4*>(out));
     return hipGetLastError();
 }
 

@@ -209,33 +209,33 @@ unsigned grid_for(size_t total) {
 
 hipError_t launch_noise(const DevView& v, uint64_t seed, hipStream_t s) {
     const size_t total = (size_t)v.n * v.n * v.T;
-    hipLaunchKernelGGL(k_noise, dim3(grid_for(total)), dim3(256), 0, s, const_cast<float2*>(v.noise), v.n, v.T, seed);
+    launch(k_noise, dim3(grid_for(total)), dim3(256), 0, s, const_cast<float2*>(v.noise), v.n, v.T, seed);
     return hipGetLastError();
 }
 
 hipError_t launch_init_spectrum(const DevView& v, const SpectrumParams& sp, hipStream_t s) {
     Sp p{sp.wind_speed, sp.gravity, sp.fetch, sp.depth, sp.wind_dir_x, sp.wind_dir_y};
-    hipLaunchKernelGGL(k_init_spectrum, dim3(grid_for((size_t)v.n * v.n * v.units)), dim3(256), 0, s, v, p);
+    launch(k_init_spectrum, dim3(grid_for((size_t)v.n * v.n * v.units)), dim3(256), 0, s, v, p);
     return hipGetLastError();
 }
 
 hipError_t launch_conjugate(const DevView& v, hipStream_t s) {
-    hipLaunchKernelGGL(k_conjugate, dim3(grid_for((size_t)v.n * v.n * v.units)), dim3(256), 0, s, v);
+    launch(k_conjugate, dim3(grid_for((size_t)v.n * v.n * v.units)), dim3(256), 0, s, v);
     return hipGetLastError();
 }
 
 hipError_t launch_evolve(const DevView& v, float t, hipStream_t s) {
-    hipLaunchKernelGGL(k_evolve, dim3(grid_for((size_t)v.n * v.n * v.units)), dim3(256), 0, s, v, t);
+    launch(k_evolve, dim3(grid_for((size_t)v.n * v.n * v.units)), dim3(256), 0, s, v, t);
     return hipGetLastError();
 }
 
 hipError_t launch_foam_import(const DevView& v, hipStream_t s) {
-    hipLaunchKernelGGL(k_foam_import, dim3(grid_for((size_t)v.n * v.n * v.units)), dim3(256), 0, s, v);
+    launch(k_foam_import, dim3(grid_for((size_t)v.n * v.n * v.units)), dim3(256), 0, s, v);
     return hipGetLastError();
 }
 
 hipError_t launch_fill(const DevView& v, hipStream_t s) {
-    hipLaunchKernelGGL(k_fill, dim3(grid_for((size_t)v.n * v.n * v.units)), dim3(256), 0, s, v);
+    launch(k_fill, dim3(grid_for((size_t)v.n * v.n * v.units)), dim3(256), 0, s, v);
     return hipGetLastError();
 }
 
