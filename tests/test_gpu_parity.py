@@ -218,6 +218,28 @@ def test_frames_vs_oracle(n, ncasc, flags):
     ctx.close()
 
 
+@pytest.mark.parametrize("n", [1024, 4096])
+def test_shallow_frames_vs_oracle(n):
+    """Shallow water (depth 4, WaterBody.cs:14's default: the TMA correction's three branches
+    and the finite-depth dw/dk, InitialSpectrum.compute:38-43, :87-91) through the fused frame
+    at the bench size and at cfg5's N, 2 frames with foam."""
+    cas = O.SCENE_CASCADES if n == 1024 else O.SCENE_CASCADES[2:3]
+    params = O.scene_params(shallow=True)
+    ctx, (noise,) = make_ctx(n, cas, params=params)
+    O.set_threads(oracle_threads() if n >= 2048 else 1)
+    try:
+        oc = O.OracleOcean(n, params, cas, noise)
+        for t in (0.75, 1.5):
+            ctx.step(t)
+            disp, deriv, turb = oc.step(t)
+            assert_channels(ctx.read_all(oh.TEX_DISP)[..., :3], disp[..., :3], what=f"disp t={t}")
+            assert_channels(ctx.read_all(oh.TEX_DERIV), deriv, what=f"deriv t={t}")
+            assert_channels(ctx.read_all(oh.TEX_TURB), turb, what=f"turb t={t}")
+    finally:
+        O.set_threads(1)
+    ctx.close()
+
+
 @pytest.mark.parametrize("times", [(20000.0, 20000.0 + 1 / 60), (36000.0, 86400.0)])
 def test_large_time_vs_oracle(times):
     """cfg3 (4 x 1024^2) at play times of 5.5 h to a day: the phase omega*t passes 2^17 rad
@@ -348,12 +370,13 @@ def normal_fp32(deriv):
     return np.stack([-sx * inv, inv, -sz * inv, np.zeros_like(inv)], -1)
 
 
-@pytest.mark.parametrize("flags", [0, oh.F_UNFUSED])
-def test_normals_derived_output(flags):
+@pytest.mark.parametrize("n,ncasc,flags", [(128, 2, 0), (128, 2, oh.F_UNFUSED), (1024, 4, 0), (4096, 1, 0)])
+def test_normals_derived_output(n, ncasc, flags):
     """NORMAL is normal_from_deriv applied to the context's own DERIV: bit-exact against the
     fp32 restatement; DERIV itself is within 1e-5 of the oracle (as in every frame test), and
-    the normal within 1e-5 norm-relative per channel of an fp64 normal of the oracle's DERIV."""
-    n, cas = 128, O.SCENE_CASCADES[:2]
+    the normal within 1e-5 norm-relative per channel of an fp64 normal of the oracle's DERIV.
+    N = 1024 writes it in pass B3's epilogue, N = 4096 in the four-step pass C2's."""
+    cas = O.SCENE_CASCADES[:ncasc]
     ctx, (noise,) = make_ctx(n, cas, flags=flags | oh.F_NORMALS)
     ctx.step(0.5)
     got_deriv = ctx.read_all(oh.TEX_DERIV)
@@ -545,7 +568,7 @@ def _box_chain(level0):
     return out
 
 
-@pytest.mark.parametrize("n,flags", [(16, 0), (64, 0), (1024, 0), (256, oh.F_UNFUSED)])
+@pytest.mark.parametrize("n,flags", [(16, 0), (64, 0), (1024, 0), (256, oh.F_UNFUSED), (2048, 0)])
 def test_mip_chains_box_filter(n, flags):
     cas = O.SCENE_CASCADES[:2]
     ctx, _ = make_ctx(n, cas, flags=flags | oh.F_MIPS)
