@@ -105,7 +105,7 @@ __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems) void k_pass_a3(De
             // column band: rows are transformed whole, only the band's columns stored
             if (row2 < total_rows && (!BAND || (unsigned)(jj + q * NSL - v.x0) < (unsigned)v.nx)) {
                 const int u2 = row2 / N, y2 = row2 % N;
-                float2* rowp = v.tplane + (size_t)p * v.plane_stride + ((size_t)u2 * TILES * N + y2) * W;
+                float2* rowp = v.tplane + (size_t)p * v.inter_stride + ((size_t)u2 * TILES * N + y2) * W;
                 if constexpr (NSL % W == 0) {
                     // x = jj + q*NSL: x/W = jj/W + q*NSL/W, x%W = jj%W (compile-time tile stride)
                     float2* dst = rowp + (size_t)(jj / W) * N * W + (jj % W);
@@ -167,7 +167,7 @@ __global__ __launch_bounds__((WT ? WT : b3_w(N)) * N / kElems) void k_pass_b3(De
         return make_win(base + (size_t)u * N * N + x0, (unsigned)((N * N - x0) * 16));
     };
     auto load = [&](int item, int p, float2 (&d)[kElems]) {
-        const Win w = make_win(v.tplane + (size_t)p * v.plane_stride + (size_t)full(item) * TILE, TILE * 8);
+        const Win w = make_win(v.tplane + (size_t)p * v.inter_stride + (size_t)full(item) * TILE, TILE * 8);
 #pragma unroll
         for (int i = 0; i < kElems; ++i) d[i] = bload2(w, toff * 8, CT::in_dy(i) * W * 8);
     };
@@ -387,7 +387,7 @@ __global__ __launch_bounds__(N / 4) void k_pass_a4(DevView v, float time, int it
                 E::template bj<E::RL>((int)threadIdx.x + m * T, b, jj);
                 if (BAND && (unsigned)(jj + q * NSL - v.x0) >= (unsigned)v.nx) return;  // outside the column band
                 const int p = p0 + b / RB, y = (b % RB) ? y2 : y1;
-                float2* dst = v.tplane + (size_t)p * v.plane_stride + ((size_t)u * TILES * N + y) * W +
+                float2* dst = v.tplane + (size_t)p * v.inter_stride + ((size_t)u * TILES * N + y) * W +
                               (size_t)(jj / W) * N * W + (jj % W);
                 dst[(size_t)q * (NSL / W) * N * W] = val;
             };

@@ -76,7 +76,7 @@ __global__ __launch_bounds__(kSeq * (N / kL1) / kElems) void k_col4s1(DevView v,
         const int blk = item % BLKS, rest = item / BLKS;  // rest = (p * units + u) * band tiles + band tile
         const int p = rest / (v.units * bnt), ub = rest % (v.units * bnt);
         const int ut = (ub / bnt) * tiles + bt0 + ub % bnt;
-        return v.tplane + (size_t)p * v.plane_stride + (size_t)ut * TILE + blk * (kSeq / kWT) * kWT;
+        return v.tplane + (size_t)p * v.inter_stride + (size_t)ut * TILE + blk * (kSeq / kWT) * kWT;
     };
     float2 cur[kElems], nxt[kElems];
     auto load = [&](int item, float2 (&d)[kElems]) {
@@ -134,7 +134,7 @@ __global__ __launch_bounds__(kSeq * kL1 / kElems) void k_col4s2(DevView v, int i
     auto full = [&](int ub) { return (ub / bnt) * tiles + bt0 + ub % bnt; };
     auto load = [&](int item, int p, float2 (&d)[kElems]) {
         const int blk = item % BLKS, ut = full(item / BLKS);
-        const float2* src = v.tplane + (size_t)p * v.plane_stride + (size_t)ut * TILE +
+        const float2* src = v.tplane + (size_t)p * v.inter_stride + (size_t)ut * TILE +
                             (size_t)kL1 * (blk * K0B + k0l) * kWT + col + lj * kWT;
 #pragma unroll
         for (int i = 0; i < kElems; ++i) d[i] = src[CT::in_dy(i) * kWT];

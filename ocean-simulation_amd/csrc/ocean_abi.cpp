@@ -68,6 +68,8 @@ struct ocean_ctx {
     long chunk_mib = 192;    // OCEAN_CHUNK_MIB: intermediate MiB per unit chunk (step_fused)
     int c4_bands = 0;        // OCEAN_C4_BANDS: N >= 2048 column passes per (unit, band); 0 = auto
     int chunk_min = 1 << 30; // OCEAN_CHUNK_MIN: units per chunk when one unit exceeds OCEAN_CHUNK_MIB
+    int chunk_reuse = 1;     // OCEAN_CHUNK_REUSE=0: one intermediate region per unit (A/B)
+    size_t inter_units = 0;  // units the intermediate holds (a chunk's, or all with chunk_reuse = 0)
     int band_x0 = 0, band_nx = 0;  // column band of the fused passes (ocean_set_column_band); nx = n: whole
     int tile_w = 8;                // column-tile width of the fused path's tile-major layouts (ocean_create)
     float4* waves = nullptr;
@@ -119,6 +121,7 @@ struct ocean_ctx {
         v.waves = waves;
         for (int p = 0; p < 4; ++p) v.plane[p] = plane[p];
         v.plane_stride = texels() * units();
+        v.inter_stride = texels() * inter_units;
         v.disp = disp;
         v.deriv = deriv;
         v.turb = turb;
@@ -262,6 +265,10 @@ void free_all(ocean_ctx* c) {
 
 }  // namespace
 
+namespace {
+int chunk_units(const ocean_ctx* ctx);
+}  // namespace
+
 extern "C" {
 
 const char* ocean_last_error(void) { return g_last_error.c_str(); }
@@ -306,6 +313,7 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
     if (const char* kc = std::getenv("OCEAN_CHUNK_MIB")) c->chunk_mib = std::atol(kc);
     if (const char* kb = std::getenv("OCEAN_C4_BANDS")) c->c4_bands = std::max(0, std::atoi(kb));
     if (const char* km = std::getenv("OCEAN_CHUNK_MIN")) c->chunk_min = std::max(1, std::atoi(km));
+    if (const char* kr = std::getenv("OCEAN_CHUNK_REUSE")) c->chunk_reuse = std::atoi(kr);
     // Width of the fused path's column tiles.  With fewer tiles than CUs (one 512^2
     // cascade: 32 tiles of 16 columns) pass B ran on an eighth of the chip, so small
     // jobs at N <= 512 take 4-column tiles (at N = 1024 pass A's
@@ -342,7 +350,8 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
         ok = ok && alloc((void**)&c->turb, tex * U * 16);
         ok = ok && alloc((void**)&c->foam, tex * U * 4);
     }
-    ok = ok && alloc((void**)&c->tplane, tex * U * 8 * c->P);
+    c->inter_units = c->chunk_reuse ? (size_t)chunk_units(c) : U;
+    ok = ok && alloc((void**)&c->tplane, tex * c->inter_units * 8 * c->P);
     if (flags & OCEAN_F_NORMALS) ok = ok && alloc((void**)&c->normal, tex * U * 16);
     if (flags & OCEAN_F_MIPS) {
         for (int l = 1; (n >> l) >= 1; ++l) c->mip_chain += (size_t)(n >> l) * (n >> l);
@@ -550,7 +559,7 @@ int ocean_step(ocean_ctx* ctx, float time) {
 
 namespace {
 // View of units [u0, u0 + nu) (unit u of the view is cascade (c0 + u) % C).
-ocean::DevView sub_view(const ocean::DevView& v, int u0, int nu) {
+ocean::DevView sub_view(const ocean::DevView& v, int u0, int nu, bool inter_at_base = false) {
     ocean::DevView s = v;
     const size_t off = (size_t)u0 * v.n * v.n;
     s.units = nu;
@@ -558,7 +567,9 @@ ocean::DevView sub_view(const ocean::DevView& v, int u0, int nu) {
     s.h0 = v.h0 + off;
     s.waves = v.waves + off;
     if (v.h0k) s.h0k = v.h0k + off;
-    s.tplane = v.tplane + off;  // plane_stride unchanged: planes stay U * N * N apart
+    // plane_stride unchanged: planes stay U * N * N apart.  inter_at_base: the chunk's
+    // intermediate starts at the base of every plane (one region reused by every chunk)
+    s.tplane = inter_at_base ? v.tplane : v.tplane + off;
     if (v.foam) s.foam = v.foam + off;
     s.disp = v.disp + off;
     if (v.deriv) s.deriv = v.deriv + off;
@@ -605,7 +616,7 @@ int step_fused(ocean_ctx* ctx, float time) {
     const ocean::DevView v = ctx->view();
     const int U = (int)ctx->units(), K = chunk_units(ctx);
     for (int u0 = 0; u0 < U; u0 += K) {
-        const ocean::DevView c = (K >= U) ? v : sub_view(v, u0, std::min(K, U - u0));
+        const ocean::DevView c = (K >= U) ? v : sub_view(v, u0, std::min(K, U - u0), ctx->inter_units < ctx->units());
         if (int r = timed(ctx, 0, [&] {
                 if (ctx->a4 && ctx->h0k_valid) return ocean::launch_pass_a_v4(c, time, ctx->stream);
                 return ocean::launch_pass_a_v3(c, time, ctx->stream);

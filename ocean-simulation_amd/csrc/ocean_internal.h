@@ -57,7 +57,11 @@ struct DevView {
     const float* casc;    // [C][5] wavelength, cutoff_low, cutoff_high, swell, fade (device)
     float gravity;        // for the per-frame wave-data recompute (fused row pass)
     int tile_w;           // width W of the tile-major layouts below: inter_w(N), or 4 for small jobs
-    float2* tplane;       // fused intermediate, P planes x [U][N/W][N][W] (tile-major), stride plane_stride
+    float2* tplane;       // fused intermediate, P planes x [K][N/W][N][W] (tile-major), stride inter_stride;
+                          // K = the units of one chunk of a frame (ocean_abi.cpp chunk_units): every chunk
+                          // reuses the same region, so its lines are rewritten in the Infinity Cache
+                          // instead of being written back to HBM once per unit
+    size_t inter_stride;  // elements between consecutive planes of tplane (K * N * N)
     float* foam;          // foam state, [U][N/W][N][W] (tile-major); TURB is its broadcast RGBA image
     float4* deriv_mips;   // OCEAN_F_MIPS: per slice, levels 1..log2 N concatenated (mip_chain texels)
     float4* turb_mips;
