@@ -1,0 +1,424 @@
+// The fused frame through a THREE-plane intermediate (N = 512 / 1024, full outputs):
+// pass AQ (mirror-pair rows) and pass BQ (column tiles).  DESIGN.md section 3, "Q schedule".
+//
+// The reference transforms four packed planes (TimeDependentSpectrum.compute:42-45):
+//   P1 = Dx + i Dz,  P2 = Dy + i Dxz,  P3 = Dyx + i Dyz,  P4 = Dxx + i Dzz
+// and keeps the real / imaginary parts of each 2D IFFT T[.] (ResultTexturesFiller.compute:20-26).
+// Re T[P] = T[herm P] and Im T[P] = T[anti P] / i, with herm P(k) = (P(k) + conj P(-k)) / 2 and
+// anti P(k) = (P(k) - conj P(-k)) / 2 (-k = the mirror texel, InitialSpectrum.compute:139).
+// Three of the four transforms the fill needs are therefore transforms of planes pass A can form
+// per texel pair (k, -k), and the fourth differs from i kz P1 only on the two Nyquist lines:
+//   Q1 = P1                         T[Q1]  = Dx  + i Dz
+//   Q2 = herm P2 + i herm P3        T[Q2]  = Dy  + i Dyx
+//   Q3 = -i anti P3 + i herm P4     T[Q3]  = Dyz + i Dxx
+//   Q4 = -i anti P2 + anti P4       T[Q4]  = Dxz + i Dzz
+// Off the lines nx = 0 and nz = 0, Q4 = i kz Q1 exactly in real arithmetic (Dxz = i kz Dx and
+// Dzz = i kz Dz texel by texel), and kz is constant along a row, so after the row transform R:
+//   R[Q4](x, y) = i kz(y) R[Q1](x, y) + d0(y)        (y != 0; d0(y) = Q4 - i kz Q1 at texel nx = 0)
+//   R[Q4](x, 0) = srow(x) = R[Q4 of row 0](x)        (row nz = 0 transformed by pass A)
+// The planes Q1..Q3 (24 B / texel instead of 32) plus the per-unit side arrays d0 and srow are the
+// whole intermediate; pass B forms R[Q4] from R[Q1] on load.  The outputs equal the four-plane
+// frame's in real arithmetic, Nyquist lines included; in fp32 they differ by rounding only.
+#include "fft_engine.h"
+#include "spectrum_math.h"
+
+#ifndef OCEAN_AQ_WPEU
+#define OCEAN_AQ_WPEU 0  // waves per SIMD pass AQ is compiled for (0: the compiler's choice; A/B builds)
+#endif
+#ifndef AQ_SKIP
+#define AQ_SKIP 1  // pass AQ's idle pass-1 waves skip the stages (A/B builds)
+#endif
+#if OCEAN_AQ_WPEU
+#define AQ_WPEU __attribute__((amdgpu_waves_per_eu(OCEAN_AQ_WPEU)))
+#else
+#define AQ_WPEU
+#endif
+
+namespace ocean {
+namespace {
+
+// (a + conj b) / 2 and (a - conj b) / 2
+__device__ __forceinline__ float2 hsum(float2 a, float2 b) { return make_float2((a.x + b.x) * 0.5f, (a.y - b.y) * 0.5f); }
+__device__ __forceinline__ float2 hdif(float2 a, float2 b) { return make_float2((a.x - b.x) * 0.5f, (a.y + b.y) * 0.5f); }
+
+struct QTex {
+    float2 q[3];
+};
+
+// Q1..Q3 at k (a) and at -k (b) from the reference planes P(k) = o, P(-k) = om.
+__device__ __forceinline__ void q_planes(const Planes4& o, const Planes4& om, QTex& a, QTex& b) {
+    const float2 h2 = hsum(o.p[1], om.p[1]), h3 = hsum(o.p[2], om.p[2]);
+    const float2 a3 = hdif(o.p[2], om.p[2]), h4 = hsum(o.p[3], om.p[3]);
+    a.q[0] = o.p[0];
+    b.q[0] = om.p[0];
+    a.q[1] = make_float2(h2.x - h3.y, h2.y + h3.x);  // h2 + i h3
+    b.q[1] = make_float2(h2.x + h3.y, h3.x - h2.y);  // conj h2 + i conj h3
+    a.q[2] = make_float2(a3.y - h4.y, h4.x - a3.x);  // i (h4 - a3)
+    b.q[2] = make_float2(a3.y + h4.y, a3.x + h4.x);  // i conj (a3 + h4)
+}
+
+// Q4(k) - i kz(k) P1(k), nonzero only on the Nyquist lines (see the header).
+__device__ __forceinline__ float2 q4_minus(const Planes4& o, const Planes4& om, float kz) {
+    const float2 a2 = hdif(o.p[1], om.p[1]), a4 = hdif(o.p[3], om.p[3]);
+    // -i a2 + a4 - i kz p1
+    return make_float2(a2.y + a4.x + kz * o.p[0].y, -a2.x + a4.y - kz * o.p[0].x);
+}
+// Q4(k) itself (row nz = 0, whose transform is srow)
+__device__ __forceinline__ float2 q4_full(const Planes4& o, const Planes4& om) {
+    const float2 a2 = hdif(o.p[1], om.p[1]), a4 = hdif(o.p[3], om.p[3]);
+    return make_float2(a2.y + a4.x, -a2.x + a4.y);
+}
+
+// Side arrays of unit u (of the chunk the view covers): d0 [N], then srow [N].
+__device__ __forceinline__ float2* q_side(const DevView& v, int u) {
+    return v.tplane + 3 * v.inter_stride + (size_t)u * 2 * v.n;
+}
+
+// Pass AQ: mirror-pair row pass writing Q1..Q3 (the structure of k_pass_a4, fft3.hip).  Item i
+// of a unit (0 <= i <= N/2) is row y1 = i with its mirror row y2 = (N - i) % N; items 0 and N/2
+// are self-mirror rows (y2 = y1), run by the same code: their second sequences duplicate the
+// first and are not stored, except that item 0 carries srow in its second Q3 slot.  Lane j
+// evolves texels x = j + r N/4 of row y1 with their mirrors (N - x) % N in row y2 and holds
+// stage-0 butterfly j of row y1 and jm = (N/4 - j) % (N/4) of row y2.  LDS pass 0: Q1, Q2 of both
+// rows; pass 1: Q3 of both rows (two of its four sequence slots idle).
+template <int N, bool BAND = false, int WT = 0>
+__global__ __launch_bounds__(N / 4) AQ_WPEU void k_pass_aq(DevView v, float time, int items) {
+    constexpr int R0 = 4, NJ = N / R0;
+    constexpr int IPU = N / 2 + 1;  // items per unit
+    using TW = StageTw<N, R0>;
+    using E = Engine<N, 4, false, true, R0, TW, kElems>;
+    constexpr int T = E::THREADS;
+    static_assert(T == NJ && E::R0 == R0, "lane j <-> stage-0 butterfly j");
+    constexpr int W = WT ? WT : inter_w(N);
+    constexpr int TILES = N / W;
+    constexpr int NSL = N / E::RL;
+    static_assert(NSL % W == 0, "tile-major emit");
+    __shared__ float2 lds[E::LDS_ELEMS];
+    __shared__ float2 twl[TW::kLdsEntries];
+    TW::load(twl, v.tw, threadIdx.x, T);
+    const float2* tws = TW::table(twl, v.tw);
+    __shared__ WaveBand band[kMaxCascades];
+    if ((int)threadIdx.x < v.C) band[threadIdx.x] = wave_band(v.casc + threadIdx.x * 5);
+    const int j = (int)threadIdx.x;
+    const int jm = (NJ - j) & (NJ - 1);
+    const bool j0 = (j == 0);
+    auto rows_of = [&](int it, int& u, int& y1, int& y2) {
+        u = it / IPU;
+        y1 = it - u * IPU;
+        y2 = (N - y1) & (N - 1);
+    };
+    auto load_pair = [&](int it, float2 (&a)[R0], float2 (&b)[R0]) {
+        int u, y1, y2;
+        rows_of(it, u, y1, y2);
+        const float2* r1 = v.h0k + ((size_t)u * N + y1) * N;
+        const float2* r2 = v.h0k + ((size_t)u * N + y2) * N;
+#pragma unroll
+        for (int r = 0; r < R0; ++r) {
+            a[r] = r1[j + r * NJ];
+            b[r] = r2[(N - j - r * NJ) & (N - 1)];
+        }
+    };
+    auto unmirror = [&](const float2* mir, float2* out) {
+#pragma unroll
+        for (int r2 = 0; r2 < R0; ++r2) out[r2] = j0 ? mir[(R0 - r2) & (R0 - 1)] : mir[R0 - 1 - r2];
+    };
+    auto put = [&](int b, int jb, const float2* x) {
+        float2* dst = lds + E::lidx(b, jb * R0);
+#pragma unroll
+        for (int q = 0; q < R0; ++q) dst[E::loff(q, 1)] = x[q];
+    };
+    float2 A[R0], B[R0], An[R0], Bn[R0];
+    int it = blockIdx.x;
+    if (it < items) load_pair(it, A, B);
+    __syncthreads();  // twiddles, band
+    for (; it < items; it += gridDim.x) {
+        const int next = it + gridDim.x;
+        if (next < items) load_pair(next, An, Bn);
+        int u, y1, y2;
+        rows_of(it, u, y1, y2);
+        const WaveBand wb = band[(u + v.c0) % v.C];
+        const bool self = (y1 == y2);
+        // after stage 0: g = (Q1 y1, Q1 y2, Q2 y1, Q2 y2, Q3 y1, Q3 y2 | row 0: srow's input)
+        float2 g[6][R0];
+        {
+            float2 mir[3][R0];
+#pragma unroll
+            for (int r = 0; r < R0; ++r) {
+                const float4 wd = wave_data(j + r * NJ, y1, N, wb, v.gravity);
+                const float2 h = evolve_h(make_float4(A[r].x, A[r].y, B[r].x, -B[r].y), evolve_phase(wd.w, time));
+                // mirror: kx -> -kx and kz -> -kz except on the Nyquist column x = 0 / row y = 0
+                const float4 wm = make_float4((j0 && r == 0) ? wd.x : -wd.x, wd.y, y1 ? -wd.z : wd.z, wd.w);
+                const Planes4 o = planes_of(h, wd), om = planes_of(make_float2(h.x, -h.y), wm);
+                QTex qa, qb;
+                q_planes(o, om, qa, qb);
+#pragma unroll
+                for (int p = 0; p < 3; ++p) {
+                    g[2 * p][r] = qa.q[p];
+                    mir[p][r] = qb.q[p];
+                }
+                if (y1 == 0) mir[2][r] = q4_full(o, om);
+                if (r == 0 && j0) {  // texel nx = 0 of both rows: d0
+                    float2* side = q_side(v, u);
+                    side[y1] = q4_minus(o, om, wd.z);
+                    side[y2] = q4_minus(om, o, wm.z);
+                }
+            }
+            unmirror(mir[0], g[1]);
+            unmirror(mir[1], g[3]);
+            unmirror(mir[2], g[5]);
+            if (y1 == 0) {  // srow's input stays in natural order (butterfly j)
+#pragma unroll
+                for (int r = 0; r < R0; ++r) g[5][r] = mir[2][r];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 6; ++k) Idft<R0>::run(g[k]);
+#pragma unroll
+        for (int ps = 0; ps < 2; ++ps) {
+            if (ps == 0) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) put(k, (k & 1) ? jm : j, g[k]);
+            } else {
+                put(0, j, g[4]);
+                put(1, y1 ? jm : j, g[5]);
+            }
+            __syncthreads();
+            auto emit = [&](int m, int q, float2 val) {
+                int b, jj;
+                E::template bj<E::RL>((int)threadIdx.x + m * T, b, jj);
+                const int p = ps == 0 ? (b >> 1) : 2;
+                const int s = b & 1;
+                if (ps == 1 && b >= 2) return;  // idle slots
+                const int x = jj + q * NSL;
+                if (s && self) {  // self-mirror row: a duplicate, or row 0's srow
+                    if (p == 2 && y1 == 0) q_side(v, u)[N + x] = val;
+                    return;
+                }
+                if (BAND && (unsigned)(x - v.x0) >= (unsigned)v.nx) return;  // outside the column band
+                float2* dst = v.tplane + (size_t)p * v.inter_stride + ((size_t)u * TILES * N + (s ? y2 : y1)) * W +
+                              (size_t)(jj / W) * N * W + (jj % W);
+                dst[(size_t)q * (NSL / W) * N * W] = val;
+            };
+            // pass 1 at N = 1024 (wave-private stages, wave w = sequence w): waves 2, 3 idle
+            if (!(AQ_SKIP && E::wave_private(1) && ps == 1 && (int)threadIdx.x >= 128))
+                E::template stages_from<1>(lds, tws, emit);
+            __syncthreads();
+        }
+#pragma unroll
+        for (int r = 0; r < R0; ++r) {
+            A[r] = An[r];
+            B[r] = Bn[r];
+        }
+    }
+}
+
+// Pass BQ: per (unit, W-column tile), four column transforms from three planes:
+//   step 0: R[Q2] -> (Dy, Dyx)          kept (LDS)
+//   step 1: R[Q1] -> (Dx, Dz)           DISP = (Dx, Dy, Dz, 1); Dyx moves to registers; before the
+//                                       transform R[Q4] = i kz R[Q1] + d0 (row 0: srow) is formed
+//                                       from the same registers into the next ring slot
+//   step 2: R[Q4] -> (Dxz, Dzz)         kept (LDS)
+//   step 3: R[Q3] -> (Dyz, Dxx)         foam (Dxx, Dzz, Dxz), TURB, DERIV = (Dyx, Dyz, Dxx, Dzz)
+// Three tile loads per item run through a three-slot register ring (two steps ahead), as in
+// k_pass_b3; d0 is staged through LDS.
+template <int N, bool BAND = false, int WT = 0>
+__global__ __launch_bounds__((WT ? WT : b3_w(N)) * N / kElems) void k_pass_bq(DevView v, int items) {
+    using CT = ColTile<N, WT ? WT : b3_w(N)>;
+    using E = typename CT::E;
+    using TW = typename CT::TW;
+    constexpr int W = CT::W;
+    constexpr int T = CT::T;
+    constexpr int RL = CT::RL;
+    constexpr int TILE = W * N;
+    constexpr bool kKeepLds = (E::LDS_ELEMS + TW::kLdsEntries + kElems * T + N) * 8 <= 160 * 1024;
+    __shared__ float2 lds[E::LDS_ELEMS];
+    __shared__ float2 twl[TW::kLdsEntries];
+    __shared__ float2 keep_lds[kKeepLds ? kElems * T : 1];
+    __shared__ float dks[kMaxCascades];
+    __shared__ float2 d0s[N];  // the item's d0, staged through LDS instead of 16 registers per lane
+    constexpr int DPL = (N + T - 1) / T;  // d0 entries each lane stages
+    TW::load(twl, v.tw, threadIdx.x, T);
+    const float2* tws = TW::table(twl, v.tw);
+    if ((int)threadIdx.x < v.C) dks[threadIdx.x] = wave_band(v.casc + threadIdx.x * 5).dk;
+    const int lb = CT::lane_b(), lj = CT::lane_j();
+    const int toff = lj * W + lb;
+    const int voff16 = (lj * N + lb) * 16;
+
+    float2 keep_reg[kKeepLds ? 1 : kElems];
+    auto kput = [&](int i, float2 x) {
+        if constexpr (kKeepLds) keep_lds[i * T + threadIdx.x] = x;
+        else keep_reg[i] = x;
+    };
+    auto kget = [&](int i) -> float2 {
+        if constexpr (kKeepLds) return keep_lds[i * T + threadIdx.x];
+        else return keep_reg[i];
+    };
+    // item -> full tile index u * tiles + tile over the column band's tiles
+    const int bt0 = v.x0 / W, bnt = v.nx / W;
+    auto full = [&](int item) { return BAND ? (item / bnt) * CT::tiles + bt0 + item % bnt : item; };
+    auto win16 = [&](const float4* base, int ft) {
+        const int u = ft / CT::tiles, x0 = (ft % CT::tiles) * W;
+        return make_win(base + (size_t)u * N * N + x0, (unsigned)((N * N - x0) * 16));
+    };
+    auto load = [&](int item, int p, float2 (&d)[kElems]) {
+        const Win w = make_win(v.tplane + (size_t)p * v.inter_stride + (size_t)full(item) * TILE, TILE * 8);
+#pragma unroll
+        for (int i = 0; i < kElems; ++i) d[i] = bload2(w, toff * 8, CT::in_dy(i) * W * 8);
+    };
+
+    float2 cur[kElems], nxt[kElems], nx2[kElems], dd[DPL], srow = make_float2(0.0f, 0.0f);
+    float kreg[kElems];
+    int item = blockIdx.x;
+    if (item < items) {
+        load(item, 1, cur);  // R[Q2]
+        load(item, 0, nxt);  // R[Q1]
+    }
+    __syncthreads();
+    for (; item < items; item += gridDim.x) {
+        const int ft = full(item);
+        const int u = ft / CT::tiles;
+        const int x0 = (ft % CT::tiles) * W;
+        const float dk = dks[(u + v.c0) % v.C];
+        float* foam = v.foam + (size_t)ft * TILE + toff;
+        float fb[kElems];
+        const bool more = item + (int)gridDim.x < items;
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+            if (st == 0) {  // side values for step 1: the unit's d0 and, on row-0 lanes, srow
+                const float2* side = q_side(v, u);
+#pragma unroll
+                for (int k = 0; k < DPL; ++k)
+                    if (k * T + (int)threadIdx.x < N) dd[k] = side[k * T + threadIdx.x];
+                if (lj == 0) srow = side[N + x0 + lb];
+                load(item, 2, nx2);  // R[Q3]
+            } else if (st == 1) {
+                // R[Q4] = i kz R[Q1] + d0 (row 0: srow) into the free ring slot
+#pragma unroll
+                for (int r = 0; r < kElems; ++r) {
+                    const int y = lj + CT::in_dy(r);
+                    const float kz = (float)(y - N / 2) * dk;
+                    const float2 c = cur[r], d = d0s[y];
+                    nx2[r] = make_float2(d.x - kz * c.y, d.y + kz * c.x);
+                }
+                if (lj == 0) nx2[0] = srow;
+            } else {
+                if (st == 2) {  // foam state for step 3, ahead of this step's prefetch
+                    const Win rf = make_win(v.foam + (size_t)ft * TILE, TILE * 4);
+#pragma unroll
+                    for (int m = 0; m < kElems / RL; ++m)
+#pragma unroll
+                        for (int q = 0; q < RL; ++q) fb[m * RL + q] = bload1(rf, toff * 4, CT::out_dy(m, q) * W * 4);
+                }
+                if (more) load(item + gridDim.x, st == 2 ? 1 : 0, nx2);  // next item's R[Q2], R[Q1]
+            }
+            const Win wd = win16(v.disp, ft), wt = win16(v.turb, ft), wv = win16(v.deriv, ft);
+            auto emit = [&](int m, int q, float2 val) {
+                const int i = m * RL + q;
+                const int dy = CT::out_dy(m, q);
+                const float s = perm_sign(x0 + lb, lj + dy);
+                const float re = val.x * s, im = val.y * s;
+                const int so = dy * N * 16;
+                if (st == 0) {  // (Dy, Dyx)
+                    kput(i, make_float2(re, im));
+                } else if (st == 1) {  // (Dx, Dz): DISP
+                    const float2 k = kget(i);
+                    gstore4_nt(make_float4(re, k.x, im, 1.0f), wd, voff16, so);
+                    kreg[i] = k.y;
+                } else if (st == 2) {  // (Dxz, Dzz)
+                    kput(i, make_float2(re, im));
+                } else {  // (Dyz, Dxx): foam, TURB, DERIV, NORMAL
+                    const float2 k = kget(i);  // (Dxz, Dzz)
+                    const float f = foam_update(fb[i], im, k.y, k.x);
+                    foam[dy * W] = f;
+                    gstore4_nt(make_float4(f, f, f, f), wt, voff16, so);
+                    gstore4_nt(make_float4(kreg[i], re, im, k.y), wv, voff16, so);
+                    if (v.normals) gstore4_nt(normal_from_deriv(kreg[i], re, im, k.y), win16(v.normal, ft), voff16, so);
+                }
+            };
+            E::run_regs(cur, lds, tws, emit);
+            if (st == 0) {
+#pragma unroll
+                for (int k = 0; k < DPL; ++k)
+                    if (k * T + (int)threadIdx.x < N) d0s[k * T + threadIdx.x] = dd[k];
+            }
+            // ring: after step 1 the formed R[Q4] (nx2) goes first and R[Q3] (nxt) stays next
+#pragma unroll
+            for (int i = 0; i < kElems; ++i) {
+                if (st == 1) {
+                    cur[i] = nx2[i];
+                } else {
+                    cur[i] = nxt[i];
+                    nxt[i] = nx2[i];
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+int num_cus_q() {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+    }
+    return cus;
+}
+
+template <class K>
+int grid_q(K kernel, int threads, int items) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0) != hipSuccess || per_cu <= 0)
+        per_cu = 1;
+    const int g = num_cus_q() * per_cu;
+    return items < g ? items : g;
+}
+
+template <int N, bool BAND = false, int WT = 0>
+hipError_t go_aq(const DevView& v, float t, hipStream_t s) {
+    if constexpr (WT == 0) {
+        if (v.tile_w != inter_w(N)) return go_aq<N, BAND, 4>(v, t, s);
+    }
+    if constexpr (!BAND) {
+        if (v.nx != N) return go_aq<N, true, WT>(v, t, s);
+    }
+    constexpr int T = N / 4;
+    const int items = v.units * (N / 2 + 1);
+    const int g = grid_q(k_pass_aq<N, BAND, WT>, T, items);
+    launch((k_pass_aq<N, BAND, WT>), dim3(g), dim3(T), 0, s, v, t, items);
+    return hipGetLastError();
+}
+
+template <int N, bool BAND = false, int WT = 0>
+hipError_t go_bq(const DevView& v, hipStream_t s) {
+    if constexpr (WT == 0) {
+        if (v.tile_w != inter_w(N)) return go_bq<N, BAND, 4>(v, s);
+    }
+    if constexpr (!BAND) {
+        if (v.nx != N) return go_bq<N, true, WT>(v, s);
+    }
+    constexpr int W = WT ? WT : b3_w(N);
+    constexpr int T = W * N / kElems;
+    const int items = v.units * (v.nx / W);
+    const int g = grid_q(k_pass_bq<N, BAND, WT>, T, items);
+    launch((k_pass_bq<N, BAND, WT>), dim3(g), dim3(T), 0, s, v, items);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+bool pass_q_supported(int n, int planes) { return planes == 4 && (n == 512 || n == 1024); }
+
+hipError_t launch_pass_a_q(const DevView& v, float t, hipStream_t s) {
+    if (!pass_q_supported(v.n, v.planes) || !v.h0k) return hipErrorInvalidValue;
+    return v.n == 512 ? go_aq<512>(v, t, s) : go_aq<1024>(v, t, s);
+}
+
+hipError_t launch_pass_b_q(const DevView& v, hipStream_t s) {
+    if (!pass_q_supported(v.n, v.planes)) return hipErrorInvalidValue;
+    return v.n == 512 ? go_bq<512>(v, s) : go_bq<1024>(v, s);
+}
+
+}  // namespace ocean

@@ -65,6 +65,7 @@ struct ocean_ctx {
     float2* h0k = nullptr;   // h0.xy for the mirror-pair row pass (pass_a4_supported sizes)
     bool h0k_valid = false;  // h0k matches h0 (false after ocean_write(H0): .zw may then be arbitrary)
     int a4 = 1;              // OCEAN_A4=0 selects the v3 row pass
+    int q = 1;               // OCEAN_Q=0: the four-plane fused frame where the three-plane one applies (A/B)
     long chunk_mib = 192;    // OCEAN_CHUNK_MIB: intermediate MiB per unit chunk (step_fused)
     int c4_bands = 0;        // OCEAN_C4_BANDS: N >= 2048 column passes per (unit, band); 0 = auto
     int chunk_min = 1 << 30; // OCEAN_CHUNK_MIN: units per chunk when one unit exceeds OCEAN_CHUNK_MIB
@@ -266,7 +267,7 @@ void free_all(ocean_ctx* c) {
 }  // namespace
 
 namespace {
-int chunk_units(const ocean_ctx* ctx);
+int chunk_units(const ocean_ctx* ctx, int planes);
 }  // namespace
 
 extern "C" {
@@ -310,6 +311,7 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
     c->noise_set.assign(n_tiles, false);
     c->band_nx = n;
     if (const char* ka = std::getenv("OCEAN_A4")) c->a4 = std::atoi(ka);
+    if (const char* kq = std::getenv("OCEAN_Q")) c->q = std::atoi(kq);
     if (const char* kc = std::getenv("OCEAN_CHUNK_MIB")) c->chunk_mib = std::atol(kc);
     if (const char* kb = std::getenv("OCEAN_C4_BANDS")) c->c4_bands = std::max(0, std::atoi(kb));
     if (const char* km = std::getenv("OCEAN_CHUNK_MIN")) c->chunk_min = std::max(1, std::atoi(km));
@@ -350,7 +352,11 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
         ok = ok && alloc((void**)&c->turb, tex * U * 16);
         ok = ok && alloc((void**)&c->foam, tex * U * 4);
     }
-    c->inter_units = c->chunk_reuse ? (size_t)chunk_units(c) : U;
+    // the intermediate holds a chunk of either schedule: P planes, or (three-plane frame) planes
+    // Q1..Q3 plus the per-unit side arrays in the fourth plane's room (fftq.hip)
+    c->inter_units = c->chunk_reuse ? (size_t)std::max(chunk_units(c, c->P),
+                                                       ocean::pass_q_supported(n, c->P) ? chunk_units(c, 3) : 1)
+                                    : U;
     ok = ok && alloc((void**)&c->tplane, tex * c->inter_units * 8 * c->P);
     if (flags & OCEAN_F_NORMALS) ok = ok && alloc((void**)&c->normal, tex * U * 16);
     if (flags & OCEAN_F_MIPS) {
@@ -583,11 +589,11 @@ ocean::DevView sub_view(const ocean::DevView& v, int u0, int nu, bool inter_at_b
 // (OCEAN_CHUNK_MIB of intermediate per chunk, 0 = whole frame at once).  Measured on
 // cfg4's 1024 units at 512^2 (8 MiB each): 64 MiB 37.9k, 128 MiB 40.7k, 192 MiB 43.1k,
 // 256 MiB 38.4k, unchunked 40.7k tile-frames/s.
-int chunk_units(const ocean_ctx* ctx) {
+int chunk_units(const ocean_ctx* ctx, int planes) {
     const long mib = ctx->chunk_mib;
     const int U = (int)ctx->units();
     if (mib <= 0) return U;
-    const size_t per_unit = ctx->texels() * 8 * ctx->P;
+    const size_t per_unit = ctx->texels() * 8 * planes;
     int k = (int)(((size_t)mib << 20) / per_unit);
     if (k >= ctx->C) k -= k % ctx->C;  // whole tiles when a chunk holds one
     if (k < 1) k = ctx->chunk_min;
@@ -610,13 +616,25 @@ int c4_bands(const ocean_ctx* ctx, int nx) {
     return nb;
 }
 
+// The three-plane fused frame (fftq.hip) runs where it applies: N = 512 / 1024 with full
+// outputs, the mirror-pair row pass's h0k valid.
+bool use_q(const ocean_ctx* ctx) {
+    return ctx->q && ctx->a4 && ctx->h0k_valid && ocean::pass_q_supported(ctx->n, ctx->P);
+}
+
 int step_fused(ocean_ctx* ctx, float time) {
     // pass A: mirror-pair rows (N = 512, 1024 with 4 planes and h0k valid) or per-texel
     // rows; pass B: column tiles (N <= 1024) or the four-step column passes (N >= 2048)
     const ocean::DevView v = ctx->view();
-    const int U = (int)ctx->units(), K = chunk_units(ctx);
+    const bool q = use_q(ctx);
+    const int U = (int)ctx->units(), K = std::min(chunk_units(ctx, q ? 3 : ctx->P), (int)ctx->inter_units);
     for (int u0 = 0; u0 < U; u0 += K) {
         const ocean::DevView c = (K >= U) ? v : sub_view(v, u0, std::min(K, U - u0), ctx->inter_units < ctx->units());
+        if (q) {
+            if (int r = timed(ctx, 0, [&] { return ocean::launch_pass_a_q(c, time, ctx->stream); }, "pass_a")) return r;
+            if (int r = timed(ctx, 1, [&] { return ocean::launch_pass_b_q(c, ctx->stream); }, "pass_b")) return r;
+            continue;
+        }
         if (int r = timed(ctx, 0, [&] {
                 if (ctx->a4 && ctx->h0k_valid) return ocean::launch_pass_a_v4(c, time, ctx->stream);
                 return ocean::launch_pass_a_v3(c, time, ctx->stream);
@@ -908,6 +926,13 @@ int ocean_step_bytes(ocean_ctx* ctx, uint64_t* pass_a, uint64_t* pass_b) {
         const bool a4 = ctx->a4 && ctx->h0k_valid && ocean::pass_a4_supported(ctx->n, ctx->P);
         // column band: h0 is read whole (rows are transformed whole), the rest scales with the band
         const uint64_t bt = tex / ctx->n * ctx->band_nx;
+        if (use_q(ctx)) {
+            // three-plane frame: pass A h0k -> Q1..Q3; pass B Q1..Q3 + foam state -> outputs
+            // (pass B's second read of Q1 is an L2 re-read; the side arrays are 16 B per row)
+            *pass_a = tex * 8 + bt * 24;
+            *pass_b = bt * (24 + 8 + outs);
+            return OCEAN_OK;
+        }
         a = tex * (a4 ? 8 : 16) + bt * 8 * P;
         b = bt * (8 * P + (full ? 8 : 0) + outs);  // + foam state read and write
         if (ocean::pass_c4_supported(ctx->n)) b += bt * 16 * P;  // four-step: step 1 reads + writes the planes

@@ -111,5 +111,10 @@ hipError_t launch_pass_c4(const DevView& v, hipStream_t s);
 // texels k and -k share wave data and the phase factor and read h0 once (h0k).
 bool pass_a4_supported(int n, int planes);
 hipError_t launch_pass_a_v4(const DevView& v, float t, hipStream_t s);
+// fftq.hip: the fused frame through a three-plane intermediate (N = 512 / 1024, full outputs,
+// whole column band): pass AQ (mirror-pair rows) + pass BQ (column tiles, four transforms).
+bool pass_q_supported(int n, int planes);
+hipError_t launch_pass_a_q(const DevView& v, float t, hipStream_t s);
+hipError_t launch_pass_b_q(const DevView& v, hipStream_t s);
 
 }  // namespace ocean

@@ -75,12 +75,15 @@ __device__ __forceinline__ Phase evolve_phase(float omega, float t) {
     sincos_fast(omega * t, &e.ey, &e.ex);
     return e;
 }
-__device__ __forceinline__ Planes4 evolve_with(float4 h, float4 w, Phase e) {
-    Planes4 o;
+// h(k, t) = ComplexMult(h0.xy, e) + ComplexMult(h0.zw, conj(e))  (:26)
+__device__ __forceinline__ float2 evolve_h(float4 h, Phase e) {
     const float ex = e.ex, ey = e.ey;
-    // ComplexMult(h0.xy, e) + ComplexMult(h0.zw, conj(e))  (:26)
-    float hx = (h.x * ex - h.y * ey) + (h.z * ex - h.w * (-ey));
-    float hy = (h.x * ey + h.y * ex) + (h.z * (-ey) + h.w * ex);
+    return make_float2((h.x * ex - h.y * ey) + (h.z * ex - h.w * (-ey)), (h.x * ey + h.y * ex) + (h.z * (-ey) + h.w * ex));
+}
+// The four packed planes of one texel from h(k, t) and its wave data (:27-45).
+__device__ __forceinline__ Planes4 planes_of(float2 h, float4 w) {
+    Planes4 o;
+    const float hx = h.x, hy = h.y;
     float ihx = -hy, ihy = hx;                                   // :27
     float ydx_x = ihx * w.x, ydx_y = ihy * w.x;                  // :29
     float ydz_x = ihx * w.z, ydz_y = ihy * w.z;                  // :30
@@ -96,6 +99,7 @@ __device__ __forceinline__ Planes4 evolve_with(float4 h, float4 w, Phase e) {
     o.p[3] = make_float2(dxdx_x - dzdz_y, dxdx_y + dzdz_x);      // :45 DxxDzz
     return o;
 }
+__device__ __forceinline__ Planes4 evolve_with(float4 h, float4 w, Phase e) { return planes_of(evolve_h(h, e), w); }
 __device__ __forceinline__ Planes4 evolve_texel(float4 h, float4 w, float t) {
     return evolve_with(h, w, evolve_phase(w.w, t));
 }

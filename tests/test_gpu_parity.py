@@ -496,15 +496,41 @@ def _ctx_with_env(env, n, cas, **kw):
 def test_mirror_pair_row_pass_bit_identical(n):
     """Pass A4 (rows y and N - y per item, texel pairs k / -k sharing wave data and
     phase) against the per-texel v3 row pass: same arithmetic per texel and per
-    butterfly, so every output bit matches (cfg3 / cfg4 shapes, 3 frames incl. foam)."""
+    butterfly, so every output bit matches (cfg3 / cfg4 shapes, 3 frames incl. foam).  Both
+    run the four-plane frame (OCEAN_Q=0)."""
     cas = O.SCENE_CASCADES
-    a, _ = _ctx_with_env({"OCEAN_A4": "1"}, n, cas)
-    b, _ = _ctx_with_env({"OCEAN_A4": "0"}, n, cas)
+    a, _ = _ctx_with_env({"OCEAN_A4": "1", "OCEAN_Q": "0"}, n, cas)
+    b, _ = _ctx_with_env({"OCEAN_A4": "0", "OCEAN_Q": "0"}, n, cas)
     for t in (0.0, 0.5, 250.0):
         a.step(t)
         b.step(t)
     for tex in (oh.TEX_DISP, oh.TEX_DERIV, oh.TEX_TURB):
         np.testing.assert_array_equal(a.read_all(tex), b.read_all(tex))
+    a.close()
+    b.close()
+
+
+@pytest.mark.parametrize("n,ncasc,shallow", [(512, 4, False), (1024, 4, False), (1024, 2, True)])
+def test_three_plane_frame_vs_four_plane(n, ncasc, shallow):
+    """The three-plane frame (fftq.hip: Q1..Q3 + the Nyquist-line side arrays) against the
+    four-plane frame of the reference's planes (OCEAN_Q=0) and against the oracle: the same
+    outputs in real arithmetic, so both within the fp32 tolerance, foam over 3 frames
+    included.  Scene cascade 0 has nonzero spectrum on the Nyquist lines, where the side
+    arrays carry the difference between Q4 and i kz Q1 (without them Dzz is off by ~1e-2)."""
+    cas = O.SCENE_CASCADES[:ncasc]
+    params = O.scene_params(shallow)
+    a, noise = _ctx_with_env({"OCEAN_Q": "1"}, n, cas, params=params)
+    b, _ = _ctx_with_env({"OCEAN_Q": "0"}, n, cas, params=params)
+    assert a.step_bytes()[0] < b.step_bytes()[0]  # the schedules differ
+    oc = O.OracleOcean(n, params, cas, noise[0])
+    for t in (0.0, 0.5, 250.0):
+        a.step(t)
+        b.step(t)
+        disp, deriv, turb = oc.step(t)
+    for tex, ref in ((oh.TEX_DISP, disp[..., :3]), (oh.TEX_DERIV, deriv), (oh.TEX_TURB, turb[..., :1])):
+        ga, gb = a.read_all(tex)[..., :ref.shape[-1]], b.read_all(tex)[..., :ref.shape[-1]]
+        assert_channels(ga, ref, what=f"Q vs oracle tex {tex}")
+        assert_channels(ga, gb, what=f"Q vs four-plane tex {tex}")
     a.close()
     b.close()
 
@@ -531,7 +557,7 @@ def test_step_bytes_follows_schedule():
     n, cas = 1024, O.SCENE_CASCADES
     ctx, _ = make_ctx(n, cas)
     tex = n * n * len(cas)
-    assert ctx.step_bytes() == (40 * tex, 88 * tex)  # pass A4 (h0k) + pass B
+    assert ctx.step_bytes() == (32 * tex, 80 * tex)  # three-plane frame: pass AQ (h0k) + pass BQ
     ctx.write(oh.TEX_H0, ctx.read(oh.TEX_H0))      # uploaded h0: pass A3 reads all of it
     assert ctx.step_bytes() == (48 * tex, 88 * tex)
     ctx.close()
@@ -718,7 +744,7 @@ def test_column_band_errors_and_bytes():
         assert e.value.code == oh.E_INVALID_ARG
     tex = n * n * len(cas)
     ctx.set_column_band(512, 512)
-    assert ctx.step_bytes() == (8 * tex + 16 * tex, 44 * tex)  # h0k read whole, the rest halves
+    assert ctx.step_bytes() == (8 * tex + 12 * tex, 40 * tex)  # h0k read whole, the rest halves (Q frame)
     ctx.close()
     u, _ = make_ctx(256, cas[:1], flags=oh.F_UNFUSED)
     with pytest.raises(oh.OceanError) as e:
