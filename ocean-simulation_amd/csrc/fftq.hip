@@ -70,9 +70,7 @@ __device__ __forceinline__ float2 q4_full(const Planes4& o, const Planes4& om) {
 }
 
 // Side arrays of unit u (of the chunk the view covers): d0 [N], then srow [N].
-__device__ __forceinline__ float2* q_side(const DevView& v, int u) {
-    return v.tplane + 3 * v.inter_stride + (size_t)u * 2 * v.n;
-}
+__device__ __forceinline__ float2* q_side(const DevView& v, int u) { return v.qside + (size_t)u * 2 * v.n; }
 
 // Pass AQ: mirror-pair row pass writing Q1..Q3 (the structure of k_pass_a4, fft3.hip).  Item i
 // of a unit (0 <= i <= N/2) is row y1 = i with its mirror row y2 = (N - i) % N; items 0 and N/2
@@ -209,6 +207,80 @@ __global__ __launch_bounds__(N / 4) AQ_WPEU void k_pass_aq(DevView v, float time
             A[r] = An[r];
             B[r] = Bn[r];
         }
+    }
+}
+
+// Pass A3Q (N = 2048 / 4096): the three-plane row pass in the shape of k_pass_a3 (fft3.hip):
+// one row per item, lane j holds texels j + r N/4 (r < 4) of four sequences, transformed
+// together: Q1, Q2, Q3 and, on row 0, srow's input (Q4 of row 0; the slot is idle on other
+// rows).  P(-k) is formed from the lane's own texel: h(-k) = conj h(k) bit for bit (h0.zw =
+// conj h0(-k) after ocean_init_spectrum), with the mirror's wave data (kx, kz negated except on
+// the Nyquist column / row).  16-wide tile-major intermediate as pass A3.
+template <int N, bool BAND = false>
+__global__ __launch_bounds__(N / 4) void k_pass_a3q(DevView v, float time, int total_rows) {
+    constexpr int FIRST = 4;
+    using TW = StageTwLds<N, FIRST>;
+    using E = Engine<N, 4, false, true, FIRST, TW>;
+    constexpr int T = E::THREADS;
+    constexpr int R0 = E::R0;
+    constexpr int NJ = N / R0;
+    constexpr int W = inter_w(N);
+    constexpr int TILES = N / W;
+    constexpr int NSL = N / E::RL;
+    static_assert(T == NJ && R0 == 4, "lane j <-> stage-0 butterfly j of each sequence");
+    __shared__ float2 lds[E::LDS_ELEMS];
+    __shared__ float2 twl[TW::kLdsEntries];
+    TW::load(twl, v.tw, threadIdx.x, T);
+    const float2* tws = TW::table(twl, v.tw);
+    __shared__ WaveBand band[kMaxCascades];
+    if ((int)threadIdx.x < v.C) band[threadIdx.x] = wave_band(v.casc + threadIdx.x * 5);
+    const int j = (int)threadIdx.x;
+    const bool j0 = (j == 0);
+    float4 h[R0];
+    auto load = [&](int item, float4* hh) {
+        const Win w = make_win(v.h0 + (size_t)item * N, (unsigned)(N * 16));
+#pragma unroll
+        for (int r = 0; r < R0; ++r) hh[r] = bload4(w, j * 16, r * NJ * 16);
+    };
+    // deal consecutive rows to one XCD (blockIdx b runs on XCD b % 8), as pass A3
+    int item = (gridDim.x % 8 == 0) ? (int)(blockIdx.x % 8) * (int)(gridDim.x / 8) + (int)blockIdx.x / 8
+                                    : (int)blockIdx.x;
+    if (item < total_rows) load(item, h);
+    __syncthreads();  // twiddles, band
+    for (; item < total_rows; item += gridDim.x) {
+        const int u = item / N, y = item % N;
+        const WaveBand wb = band[(u + v.c0) % v.C];
+        float2 in[4 * R0];  // slot p * R0 + r: sequence p, stage-0 input r
+#pragma unroll
+        for (int r = 0; r < R0; ++r) {
+            const float4 wd = wave_data(j + r * NJ, y, N, wb, v.gravity);
+            const float2 hh = evolve_h(h[r], evolve_phase(wd.w, time));
+            const float4 wm = make_float4((j0 && r == 0) ? wd.x : -wd.x, wd.y, y ? -wd.z : wd.z, wd.w);
+            const Planes4 o = planes_of(hh, wd), om = planes_of(make_float2(hh.x, -hh.y), wm);
+            QTex qa, qb;
+            q_planes(o, om, qa, qb);
+#pragma unroll
+            for (int p = 0; p < 3; ++p) in[p * R0 + r] = qa.q[p];
+            in[3 * R0 + r] = y ? make_float2(0.0f, 0.0f) : q4_full(o, om);
+            if (r == 0 && j0) q_side(v, u)[y] = q4_minus(o, om, wd.z);
+        }
+        const int next = item + gridDim.x;
+        auto emit = [&](int m, int q, float2 val) {
+            int b, jj;
+            E::template bj<E::RL>((int)threadIdx.x + m * T, b, jj);
+            const int x = jj + q * NSL;
+            if (b == 3) {
+                if (y == 0) q_side(v, u)[N + x] = val;  // srow
+                return;
+            }
+            if (BAND && (unsigned)(x - v.x0) >= (unsigned)v.nx) return;  // outside the column band
+            float2* rowp = v.tplane + (size_t)b * v.inter_stride + ((size_t)u * TILES * N + y) * W;
+            float2* dst = rowp + (size_t)(jj / W) * N * W + (jj % W);
+            dst[(size_t)q * (NSL / W) * N * W] = val;
+        };
+        E::run_regs(in, lds, tws, emit);
+        __syncthreads();
+        if (next < total_rows) load(next, h);
     }
 }
 
@@ -391,6 +463,18 @@ hipError_t go_aq(const DevView& v, float t, hipStream_t s) {
     return hipGetLastError();
 }
 
+template <int N, bool BAND = false>
+hipError_t go_a3q(const DevView& v, float t, hipStream_t s) {
+    if constexpr (!BAND) {
+        if (v.nx != N) return go_a3q<N, true>(v, t, s);
+    }
+    constexpr int T = N / 4;
+    const int total = v.units * N;
+    const int g = grid_q(k_pass_a3q<N, BAND>, T, total);
+    launch((k_pass_a3q<N, BAND>), dim3(g), dim3(T), 0, s, v, t, total);
+    return hipGetLastError();
+}
+
 template <int N, bool BAND = false, int WT = 0>
 hipError_t go_bq(const DevView& v, hipStream_t s) {
     if constexpr (WT == 0) {
@@ -409,15 +493,21 @@ hipError_t go_bq(const DevView& v, hipStream_t s) {
 
 }  // namespace
 
-bool pass_q_supported(int n, int planes) { return planes == 4 && (n == 512 || n == 1024); }
+bool pass_q_supported(int n, int planes) { return planes == 4 && n >= 512 && n <= 4096; }
 
 hipError_t launch_pass_a_q(const DevView& v, float t, hipStream_t s) {
-    if (!pass_q_supported(v.n, v.planes) || !v.h0k) return hipErrorInvalidValue;
-    return v.n == 512 ? go_aq<512>(v, t, s) : go_aq<1024>(v, t, s);
+    if (!pass_q_supported(v.n, v.planes) || !v.qside) return hipErrorInvalidValue;
+    switch (v.n) {
+        case 512: return v.h0k ? go_aq<512>(v, t, s) : hipErrorInvalidValue;
+        case 1024: return v.h0k ? go_aq<1024>(v, t, s) : hipErrorInvalidValue;
+        case 2048: return go_a3q<2048>(v, t, s);
+        case 4096: return go_a3q<4096>(v, t, s);
+    }
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch_pass_b_q(const DevView& v, hipStream_t s) {
-    if (!pass_q_supported(v.n, v.planes)) return hipErrorInvalidValue;
+    if (!pass_q_supported(v.n, v.planes) || v.n > 1024 || !v.qside) return hipErrorInvalidValue;
     return v.n == 512 ? go_bq<512>(v, s) : go_bq<1024>(v, s);
 }
 

@@ -64,6 +64,7 @@ struct ocean_ctx {
     float4* h0 = nullptr;
     float2* h0k = nullptr;   // h0.xy for the mirror-pair row pass (pass_a4_supported sizes)
     bool h0k_valid = false;  // h0k matches h0 (false after ocean_write(H0): .zw may then be arbitrary)
+    bool h0_conj = false;    // h0.zw = conj h0(-k) (from ocean_init_spectrum; the three-plane frame needs it)
     int a4 = 1;              // OCEAN_A4=0 selects the v3 row pass
     int q = 1;               // OCEAN_Q=0: the four-plane fused frame where the three-plane one applies (A/B)
     long chunk_mib = 192;    // OCEAN_CHUNK_MIB: intermediate MiB per unit chunk (step_fused)
@@ -83,6 +84,7 @@ struct ocean_ctx {
     float* casc = nullptr;
     float2* tplane = nullptr;  // fused-path intermediate (tile-major), P planes
     float* foam = nullptr;     // foam state (tile-major)
+    float2* qside = nullptr;   // three-plane frame side arrays (d0, srow per unit of a chunk)
     float4* deriv_mips = nullptr;  // OCEAN_F_MIPS chains (levels 1..log2 N per slice)
     float4* turb_mips = nullptr;
     size_t mip_chain = 0;
@@ -133,6 +135,7 @@ struct ocean_ctx {
         v.tile_w = tile_w;
         v.tplane = tplane;
         v.foam = foam;
+        v.qside = qside;
         v.deriv_mips = deriv_mips;
         v.turb_mips = turb_mips;
         v.mip_chain = mip_chain;
@@ -252,7 +255,8 @@ int slice_ptr(ocean_ctx* ctx, int tex, int tile, int cascade, size_t bytes, char
 
 void free_all(ocean_ctx* c) {
     void* ptrs[] = {c->noise, c->h0, c->h0k, c->waves, c->plane[0], c->disp, c->deriv,
-                    c->turb,  c->normal, c->tw,    c->casc,     c->tplane, c->foam, c->deriv_mips, c->turb_mips};
+                    c->turb,  c->normal, c->tw,    c->casc,     c->tplane, c->foam, c->deriv_mips, c->turb_mips,
+                    c->qside};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& t : c->pending) {
@@ -268,6 +272,8 @@ void free_all(ocean_ctx* c) {
 
 namespace {
 int chunk_units(const ocean_ctx* ctx, int planes);
+// intermediate planes of the three-plane frame: Q1..Q3, plus the four-step column passes' R[Q4]
+int q_planes(const ocean_ctx* ctx) { return ctx->n >= 2048 ? 4 : 3; }
 }  // namespace
 
 extern "C" {
@@ -355,9 +361,10 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
     // the intermediate holds a chunk of either schedule: P planes, or (three-plane frame) planes
     // Q1..Q3 plus the per-unit side arrays in the fourth plane's room (fftq.hip)
     c->inter_units = c->chunk_reuse ? (size_t)std::max(chunk_units(c, c->P),
-                                                       ocean::pass_q_supported(n, c->P) ? chunk_units(c, 3) : 1)
+                                                       ocean::pass_q_supported(n, c->P) ? chunk_units(c, q_planes(c)) : 1)
                                     : U;
     ok = ok && alloc((void**)&c->tplane, tex * c->inter_units * 8 * c->P);
+    if (ocean::pass_q_supported(n, c->P)) ok = ok && alloc((void**)&c->qside, c->inter_units * 2 * n * 8);
     if (flags & OCEAN_F_NORMALS) ok = ok && alloc((void**)&c->normal, tex * U * 16);
     if (flags & OCEAN_F_MIPS) {
         for (int l = 1; (n >> l) >= 1; ++l) c->mip_chain += (size_t)(n >> l) * (n >> l);
@@ -492,6 +499,7 @@ int ocean_init_spectrum(ocean_ctx* ctx) {
     // _TurbulenceTextures; it starts at zero (ocean_create) and ocean_reset_foam clears it
     ctx->spectrum_ready = true;
     ctx->h0k_valid = ctx->h0k != nullptr;
+    ctx->h0_conj = true;
     return OCEAN_OK;
 }
 
@@ -577,6 +585,7 @@ ocean::DevView sub_view(const ocean::DevView& v, int u0, int nu, bool inter_at_b
     // intermediate starts at the base of every plane (one region reused by every chunk)
     s.tplane = inter_at_base ? v.tplane : v.tplane + off;
     if (v.foam) s.foam = v.foam + off;
+    if (v.qside) s.qside = inter_at_base ? v.qside : v.qside + (size_t)u0 * 2 * v.n;
     s.disp = v.disp + off;
     if (v.deriv) s.deriv = v.deriv + off;
     if (v.turb) s.turb = v.turb + off;
@@ -619,7 +628,8 @@ int c4_bands(const ocean_ctx* ctx, int nx) {
 // The three-plane fused frame (fftq.hip) runs where it applies: N = 512 / 1024 with full
 // outputs, the mirror-pair row pass's h0k valid.
 bool use_q(const ocean_ctx* ctx) {
-    return ctx->q && ctx->a4 && ctx->h0k_valid && ocean::pass_q_supported(ctx->n, ctx->P);
+    if (!ctx->q || !ctx->h0_conj || !ocean::pass_q_supported(ctx->n, ctx->P)) return false;
+    return ctx->n >= 2048 || (ctx->a4 && ctx->h0k_valid);  // N <= 1024: the mirror-pair row pass reads h0k
 }
 
 int step_fused(ocean_ctx* ctx, float time) {
@@ -627,9 +637,27 @@ int step_fused(ocean_ctx* ctx, float time) {
     // rows; pass B: column tiles (N <= 1024) or the four-step column passes (N >= 2048)
     const ocean::DevView v = ctx->view();
     const bool q = use_q(ctx);
-    const int U = (int)ctx->units(), K = std::min(chunk_units(ctx, q ? 3 : ctx->P), (int)ctx->inter_units);
+    const int U = (int)ctx->units(), K = std::min(chunk_units(ctx, q ? q_planes(ctx) : ctx->P), (int)ctx->inter_units);
     for (int u0 = 0; u0 < U; u0 += K) {
         const ocean::DevView c = (K >= U) ? v : sub_view(v, u0, std::min(K, U - u0), ctx->inter_units < ctx->units());
+        if (q && ctx->n >= 2048) {
+            if (int r = timed(ctx, 0, [&] { return ocean::launch_pass_a_q(c, time, ctx->stream); }, "pass_a")) return r;
+            const int nb = c4_bands(ctx, c.nx);
+            if (nb == 1) {
+                if (int r = timed(ctx, 1, [&] { return ocean::launch_pass_c4q(c, ctx->stream); }, "pass_c")) return r;
+                continue;
+            }
+            const int w = c.nx / nb;
+            for (int u = 0; u < c.units; ++u)
+                for (int b = 0; b < nb; ++b) {
+                    ocean::DevView cb = sub_view(c, u, 1);
+                    cb.x0 = c.x0 + b * w;
+                    cb.nx = (b == nb - 1) ? c.nx - b * w : w;
+                    if (int r = timed(ctx, 1, [&] { return ocean::launch_pass_c4q(cb, ctx->stream); }, "pass_c"))
+                        return r;
+                }
+            continue;
+        }
         if (q) {
             if (int r = timed(ctx, 0, [&] { return ocean::launch_pass_a_q(c, time, ctx->stream); }, "pass_a")) return r;
             if (int r = timed(ctx, 1, [&] { return ocean::launch_pass_b_q(c, ctx->stream); }, "pass_b")) return r;
@@ -810,7 +838,10 @@ int ocean_write(ocean_ctx* ctx, int texture, int tile, int cascade, const void* 
     OCEAN_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
     OCEAN_HIP(hipStreamSynchronize(ctx->stream));
     if (texture == OCEAN_TEX_NOISE) ctx->noise_set[tile] = true;
-    if (texture == OCEAN_TEX_H0) ctx->h0k_valid = false;  // the v3 row pass reads h0 (.zw included)
+    if (texture == OCEAN_TEX_H0) {  // the v3 row pass reads h0 (.zw included); the three-plane frame
+        ctx->h0k_valid = false;     // needs .zw = conj h0(-k), which an upload need not keep
+        ctx->h0_conj = false;
+    }
     if (texture == OCEAN_TEX_TURB) {  // foam state follows the uploaded TURB.x (resume)
         const ocean::DevView v = ctx->view();
         OCEAN_HIP(ocean::launch_foam_import(v, ctx->stream));
@@ -927,10 +958,11 @@ int ocean_step_bytes(ocean_ctx* ctx, uint64_t* pass_a, uint64_t* pass_b) {
         // column band: h0 is read whole (rows are transformed whole), the rest scales with the band
         const uint64_t bt = tex / ctx->n * ctx->band_nx;
         if (use_q(ctx)) {
-            // three-plane frame: pass A h0k -> Q1..Q3; pass B Q1..Q3 + foam state -> outputs
-            // (pass B's second read of Q1 is an L2 re-read; the side arrays are 16 B per row)
-            *pass_a = tex * 8 + bt * 24;
-            *pass_b = bt * (24 + 8 + outs);
+            // three-plane frame (the side arrays, 16 B per row, not counted): pass A h0k (h0 at
+            // N >= 2048) -> Q1..Q3; pass B Q1..Q3 + foam state -> outputs, or at N >= 2048 the
+            // four-step passes: C1 reads Q1..Q3 and writes them with R[Q4], C2 reads four planes
+            *pass_a = tex * (ctx->n >= 2048 ? 16 : 8) + bt * 24;
+            *pass_b = ctx->n >= 2048 ? bt * (24 + 32 + 32 + 8 + outs) : bt * (24 + 8 + outs);
             return OCEAN_OK;
         }
         a = tex * (a4 ? 8 : 16) + bt * 8 * P;

@@ -63,6 +63,7 @@ struct DevView {
                           // instead of being written back to HBM once per unit
     size_t inter_stride;  // elements between consecutive planes of tplane (K * N * N)
     float* foam;          // foam state, [U][N/W][N][W] (tile-major); TURB is its broadcast RGBA image
+    float2* qside;        // three-plane frame (fftq.hip): per unit of a chunk, d0 [N] then srow [N]
     float4* deriv_mips;   // OCEAN_F_MIPS: per slice, levels 1..log2 N concatenated (mip_chain texels)
     float4* turb_mips;
     size_t mip_chain;     // texels per slice chain: sum over L >= 1 of (N >> L)^2
@@ -111,10 +112,14 @@ hipError_t launch_pass_c4(const DevView& v, hipStream_t s);
 // texels k and -k share wave data and the phase factor and read h0 once (h0k).
 bool pass_a4_supported(int n, int planes);
 hipError_t launch_pass_a_v4(const DevView& v, float t, hipStream_t s);
-// fftq.hip: the fused frame through a three-plane intermediate (N = 512 / 1024, full outputs,
-// whole column band): pass AQ (mirror-pair rows) + pass BQ (column tiles, four transforms).
+// fftq.hip: the fused frame through a three-plane intermediate (full outputs): pass AQ
+// (mirror-pair rows, N = 512 / 1024) or A3Q (one row per item, N = 2048 / 4096), then pass BQ
+// (column tiles, four transforms, N <= 1024) or the four-step column passes with Q planes.
 bool pass_q_supported(int n, int planes);
 hipError_t launch_pass_a_q(const DevView& v, float t, hipStream_t s);
 hipError_t launch_pass_b_q(const DevView& v, hipStream_t s);
+// fft4k.hip with the three-plane intermediate: C1 also forms and transforms R[Q4] into the fourth
+// plane slot; C2 runs the three-plane epilogue.
+hipError_t launch_pass_c4q(const DevView& v, hipStream_t s);
 
 }  // namespace ocean

@@ -510,13 +510,16 @@ def test_mirror_pair_row_pass_bit_identical(n):
     b.close()
 
 
-@pytest.mark.parametrize("n,ncasc,shallow", [(512, 4, False), (1024, 4, False), (1024, 2, True)])
+@pytest.mark.parametrize("n,ncasc,shallow", [(512, 4, False), (1024, 4, False), (1024, 2, True), (2048, 2, False),
+                                             (4096, 1, True)])
 def test_three_plane_frame_vs_four_plane(n, ncasc, shallow):
     """The three-plane frame (fftq.hip: Q1..Q3 + the Nyquist-line side arrays) against the
     four-plane frame of the reference's planes (OCEAN_Q=0) and against the oracle: the same
     outputs in real arithmetic, so both within the fp32 tolerance, foam over 3 frames
     included.  Scene cascade 0 has nonzero spectrum on the Nyquist lines, where the side
-    arrays carry the difference between Q4 and i kz Q1 (without them Dzz is off by ~1e-2)."""
+    arrays carry the difference between Q4 and i kz Q1 (without them Dzz is off by ~1e-2).  N = 2048 /
+    4096: pass A3Q and the four-step column passes forming R[Q4] in C1."""
+    O.set_threads(oracle_threads() if n >= 2048 else 1)
     cas = O.SCENE_CASCADES[:ncasc]
     params = O.scene_params(shallow)
     a, noise = _ctx_with_env({"OCEAN_Q": "1"}, n, cas, params=params)
@@ -531,6 +534,7 @@ def test_three_plane_frame_vs_four_plane(n, ncasc, shallow):
         ga, gb = a.read_all(tex)[..., :ref.shape[-1]], b.read_all(tex)[..., :ref.shape[-1]]
         assert_channels(ga, ref, what=f"Q vs oracle tex {tex}")
         assert_channels(ga, gb, what=f"Q vs four-plane tex {tex}")
+    O.set_threads(1)
     a.close()
     b.close()
 
