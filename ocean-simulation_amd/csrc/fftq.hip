@@ -25,6 +25,9 @@
 #ifndef OCEAN_AQ_WPEU
 #define OCEAN_AQ_WPEU 0  // waves per SIMD pass AQ is compiled for (0: the compiler's choice; A/B builds)
 #endif
+#ifndef OCEAN_AQ_CTW
+#define OCEAN_AQ_CTW 0  // 1: compact LDS twiddle tables in pass AQ (37.4 instead of 43.5 KiB; A/B builds)
+#endif
 #ifndef AQ_SKIP
 #define AQ_SKIP 1  // pass AQ's idle pass-1 waves skip the stages (A/B builds)
 #endif
@@ -83,7 +86,7 @@ template <int N, bool BAND = false, int WT = 0>
 __global__ __launch_bounds__(N / 4) AQ_WPEU void k_pass_aq(DevView v, float time, int items) {
     constexpr int R0 = 4, NJ = N / R0;
     constexpr int IPU = N / 2 + 1;  // items per unit
-    using TW = StageTw<N, R0>;
+    using TW = std::conditional_t<OCEAN_AQ_CTW, StageTwCompact<N, R0>, StageTw<N, R0>>;
     using E = Engine<N, 4, false, true, R0, TW, kElems>;
     constexpr int T = E::THREADS;
     static_assert(T == NJ && E::R0 == R0, "lane j <-> stage-0 butterfly j");
