@@ -11,6 +11,8 @@
 //    (fft_engine.h, memory ops);
 //  * every LDS access of a butterfly is (per-lane base) + (compile-time
 //    offset), twiddles come from per-stage LDS tables (fft_engine.h).
+#include <cstdlib>
+
 #include "fft_engine.h"
 
 namespace ocean {
@@ -64,13 +66,18 @@ __global__ __launch_bounds__(B * N / kElems) void k_rows2(float2* __restrict__ p
 }
 
 // Standalone column pass + permute, in place: item = W columns of one unit.
-// W = 16 at N = 1024 (128-byte row segments; 1024 lanes), col_tile(N) otherwise.
+// W = 16 at N = 1024 (128-byte row segments; 1024 lanes), col_tile(N) otherwise; at N = 1024 the
+// default is W = 8 with XCD-paired halves (XP below): 2 workgroups per CU instead of 1, and every
+// 128-byte line still moves through one L2.
 constexpr int cols2_w(int N) { return N == 1024 ? 16 : col_tile(N); }
 
-template <int N>
-__global__ __launch_bounds__(cols2_w(N) * N / kElems) void k_cols2(float2* __restrict__ plane, int items,
-                                                                  const float2* __restrict__ tw) {
-    using CT = ColTile<N, cols2_w(N)>;
+// XP (W = 8 at N = 1024): the two 8-column halves of a 16-column tile go to items i and i + 8,
+// which blocks b and b + 8 -- one XCD under round-robin placement (speed only, never correctness)
+// -- take at the same time, so each 128-byte line is fetched and written back through one L2.
+template <int N, int W_ = cols2_w(N), bool XP = false>
+__global__ __launch_bounds__(W_ * N / kElems) void k_cols2(float2* __restrict__ plane, int items,
+                                                          const float2* __restrict__ tw) {
+    using CT = ColTile<N, W_>;
     using E = typename CT::E;
     using TW = typename CT::TW;
     constexpr int W = CT::W;
@@ -81,8 +88,14 @@ __global__ __launch_bounds__(cols2_w(N) * N / kElems) void k_cols2(float2* __res
     const int lb = CT::lane_b(), lj = CT::lane_j();
     const int voff = (lj * N + lb) * 8;
     float2 cur[kElems], nxt[kElems];
+    // item -> tile index (unit * tiles + tile)
+    auto tile_of = [&](int item) {
+        if constexpr (XP) return (item & ~15) + 2 * (item & 7) + ((item >> 3) & 1);
+        else return item;
+    };
     auto win = [&](int item) {
-        const int u = item / CT::tiles, x0 = (item - u * CT::tiles) * W;
+        const int t = tile_of(item);
+        const int u = t / CT::tiles, x0 = (t - u * CT::tiles) * W;
         return make_win(plane + (size_t)u * N * N + x0, (unsigned)((N * N - x0) * 8));
     };
     auto load = [&](int item, float2 (&d)[kElems]) {
@@ -97,7 +110,7 @@ __global__ __launch_bounds__(cols2_w(N) * N / kElems) void k_cols2(float2* __res
         const int next = item + gridDim.x;
         if (next < items) load(next, nxt);
         const Win w = win(item);
-        const int x0 = (item % CT::tiles) * W;
+        const int x0 = (tile_of(item) % CT::tiles) * W;
         auto emit = [&](int m, int q, float2 val) {
             const int dy = CT::out_dy(m, q);
             const float s = perm_sign(x0 + lb, lj + dy);
@@ -164,13 +177,23 @@ struct Rows2 {
 };
 template <int N>
 struct Cols2 {
-    static hipError_t go(const DevView* v, int p, int np, hipStream_t s) {
-        constexpr int W = cols2_w(N);
+    template <int W, bool XP>
+    static hipError_t go_w(const DevView* v, int p, int np, hipStream_t s) {
         constexpr int T = W * N / kElems;
         const int items = np * v->units * (N / W);
-        const int g = persistent_grid(k_cols2<N>, T, items);
-        launch(k_cols2<N>, dim3(g), dim3(T), 0, s, v->plane[p], items, v->tw);
+        int g = persistent_grid(k_cols2<N, W, XP>, T, items);
+        if (XP) g -= g % 16;  // halves of a tile on blocks b, b + 8 at every step of the item loop
+        launch((k_cols2<N, W, XP>), dim3(g), dim3(T), 0, s, v->plane[p], items, v->tw);
         return hipGetLastError();
+    }
+    static hipError_t go(const DevView* v, int p, int np, hipStream_t s) {
+        if constexpr (N == 1024) {
+            // default: 8-column halves paired on one XCD (45.6 against 49.7 us for 4 x 1024^2 x 4 planes);
+            // OCEAN_COLS2_XP=0 selects the 16-column tiles (A/B)
+            static const int xp = std::getenv("OCEAN_COLS2_XP") ? std::atoi(std::getenv("OCEAN_COLS2_XP")) : 1;
+            if (xp) return go_w<8, true>(v, p, np, s);
+        }
+        return go_w<cols2_w(N), false>(v, p, np, s);
     }
 };
 template <int N>
