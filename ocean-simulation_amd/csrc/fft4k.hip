@@ -291,15 +291,10 @@ bool pass_c4_supported(int n) { return n == 2048 || n == 4096; }
 hipError_t launch_pass_c4q(const DevView& v, hipStream_t s) {
     if (v.planes != 4 || !v.qside) return hipErrorInvalidValue;
     hipError_t e = hipErrorInvalidValue;
-    switch (v.n) {
-        case 2048: e = go_c1<2048, true>(v, s); break;
-        case 4096: e = go_c1<4096, true>(v, s); break;
-    }
+    if (v.n != 4096) return hipErrorInvalidValue;  // the three-plane frame at N >= 2048 runs at 4096 only
+    e = go_c1<4096, true>(v, s);
     if (e != hipSuccess) return e;
-    switch (v.n) {
-        case 2048: return go_c2<2048, 4, true>(v, s);
-        case 4096: return go_c2<4096, 4, true>(v, s);
-    }
+    return go_c2<4096, 4, true>(v, s);
     return hipErrorInvalidValue;
 }
 

@@ -213,7 +213,7 @@ __global__ __launch_bounds__(N / 4) AQ_WPEU void k_pass_aq(DevView v, float time
     }
 }
 
-// Pass A3Q (N = 2048 / 4096): the three-plane row pass in the shape of k_pass_a3 (fft3.hip):
+// Pass A3Q (N = 4096): the three-plane row pass in the shape of k_pass_a3 (fft3.hip):
 // one row per item, lane j holds texels j + r N/4 (r < 4) of four sequences, transformed
 // together: Q1, Q2, Q3 and, on row 0, srow's input (Q4 of row 0; the slot is idle on other
 // rows).  P(-k) is formed from the lane's own texel: h(-k) = conj h(k) bit for bit (h0.zw =
@@ -496,14 +496,15 @@ hipError_t go_bq(const DevView& v, hipStream_t s) {
 
 }  // namespace
 
-bool pass_q_supported(int n, int planes) { return planes == 4 && n >= 512 && n <= 4096; }
+// N = 2048 keeps the four-plane passes: pass A3Q's idle fourth sequence slot costs more there
+// than the column passes save (4 x 2048^2: 612 against 599 us per frame).
+bool pass_q_supported(int n, int planes) { return planes == 4 && (n == 512 || n == 1024 || n == 4096); }
 
 hipError_t launch_pass_a_q(const DevView& v, float t, hipStream_t s) {
     if (!pass_q_supported(v.n, v.planes) || !v.qside) return hipErrorInvalidValue;
     switch (v.n) {
         case 512: return v.h0k ? go_aq<512>(v, t, s) : hipErrorInvalidValue;
         case 1024: return v.h0k ? go_aq<1024>(v, t, s) : hipErrorInvalidValue;
-        case 2048: return go_a3q<2048>(v, t, s);
         case 4096: return go_a3q<4096>(v, t, s);
     }
     return hipErrorInvalidValue;

@@ -510,15 +510,16 @@ def test_mirror_pair_row_pass_bit_identical(n):
     b.close()
 
 
-@pytest.mark.parametrize("n,ncasc,shallow", [(512, 4, False), (1024, 4, False), (1024, 2, True), (2048, 2, False),
+@pytest.mark.parametrize("n,ncasc,shallow", [(512, 4, False), (1024, 4, False), (1024, 2, True), (4096, 2, False),
                                              (4096, 1, True)])
 def test_three_plane_frame_vs_four_plane(n, ncasc, shallow):
     """The three-plane frame (fftq.hip: Q1..Q3 + the Nyquist-line side arrays) against the
     four-plane frame of the reference's planes (OCEAN_Q=0) and against the oracle: the same
     outputs in real arithmetic, so both within the fp32 tolerance, foam over 3 frames
     included.  Scene cascade 0 has nonzero spectrum on the Nyquist lines, where the side
-    arrays carry the difference between Q4 and i kz Q1 (without them Dzz is off by ~1e-2).  N = 2048 /
-    4096: pass A3Q and the four-step column passes forming R[Q4] in C1."""
+    arrays carry the difference between Q4 and i kz Q1 (without them Dzz is off by ~1e-2).  N = 4096:
+    pass A3Q and the four-step column passes forming R[Q4] in C1 (N = 2048 keeps the
+    four-plane passes)."""
     O.set_threads(oracle_threads() if n >= 2048 else 1)
     cas = O.SCENE_CASCADES[:ncasc]
     params = O.scene_params(shallow)
