@@ -60,6 +60,26 @@ __device__ __forceinline__ void q_planes(const Planes4& o, const Planes4& om, QT
     b.q[2] = make_float2(a3.y + h4.y, a3.x + h4.x);  // i conj (a3 + h4)
 }
 
+// Q1..Q3 at k and -k straight from h = h(k, t) and the texel's wave data w = (kx, 1/|k|, kz, .),
+// for a texel pair off the Nyquist lines (there h(-k) = conj h, and the mirror's wave data is
+// (-kx, 1/|k|, -kz)): with P1..P4 of TimeDependentSpectrum.compute:29-45,
+//   Q1 = P1 = (i kx - kz) / |k| h,  Q2 = Y + i Dyx = (1 - kx) h,  Q3 = Dyz + i Dxx = i (kz - kx^2 / |k|) h,
+// and at -k the same with kx, kz negated and conj h: a complex scale of h each, 24 VALU for the pair
+// where planes_of twice + q_planes take ~80 (pass A is VALU-bound: SQ counters).  The
+// same values in real arithmetic; in fp32 they round differently (parity tolerance, tests).
+__device__ __forceinline__ void q_fast(float2 h, float4 w, QTex& a, QTex& b) {
+    const float c1x = -w.z * w.y, c1y = w.x * w.y;  // (i kx - kz) / |k|
+    a.q[0] = make_float2(c1x * h.x - c1y * h.y, c1x * h.y + c1y * h.x);
+    b.q[0] = make_float2(-(c1x * h.x + c1y * h.y), c1x * h.y - c1y * h.x);  // -(c1) conj h
+    const float s2a = 1.0f - w.x, s2b = 1.0f + w.x;
+    a.q[1] = make_float2(s2a * h.x, s2a * h.y);
+    b.q[1] = make_float2(s2b * h.x, -s2b * h.y);
+    const float kk = w.x * w.x * w.y;
+    const float t1 = w.z - kk, t2 = -w.z - kk;
+    a.q[2] = make_float2(-t1 * h.y, t1 * h.x);  // i t1 h
+    b.q[2] = make_float2(t2 * h.y, t2 * h.x);   // i t2 conj h
+}
+
 // Q4(k) - i kz(k) P1(k), nonzero only on the Nyquist lines (see the header).
 __device__ __forceinline__ float2 q4_minus(const Planes4& o, const Planes4& om, float kz) {
     const float2 a2 = hdif(o.p[1], om.p[1]), a4 = hdif(o.p[3], om.p[3]);
@@ -147,21 +167,25 @@ __global__ __launch_bounds__(N / 4) AQ_WPEU void k_pass_aq(DevView v, float time
             for (int r = 0; r < R0; ++r) {
                 const float4 wd = wave_data(j + r * NJ, y1, N, wb, v.gravity);
                 const float2 h = evolve_h(make_float4(A[r].x, A[r].y, B[r].x, -B[r].y), evolve_phase(wd.w, time));
-                // mirror: kx -> -kx and kz -> -kz except on the Nyquist column x = 0 / row y = 0
-                const float4 wm = make_float4((j0 && r == 0) ? wd.x : -wd.x, wd.y, y1 ? -wd.z : wd.z, wd.w);
-                const Planes4 o = planes_of(h, wd), om = planes_of(make_float2(h.x, -h.y), wm);
                 QTex qa, qb;
-                q_planes(o, om, qa, qb);
+                if (y1 != 0 && !(r == 0 && j0)) {
+                    q_fast(h, wd, qa, qb);
+                } else {
+                    // Nyquist lines: the mirror keeps kx on the column x = 0 and kz on the row y = 0
+                    const float4 wm = make_float4((j0 && r == 0) ? wd.x : -wd.x, wd.y, y1 ? -wd.z : wd.z, wd.w);
+                    const Planes4 o = planes_of(h, wd), om = planes_of(make_float2(h.x, -h.y), wm);
+                    q_planes(o, om, qa, qb);
+                    if (y1 == 0) qb.q[2] = q4_full(o, om);  // row 0: srow's input in the second Q3 slot
+                    if (r == 0 && j0) {  // texel nx = 0 of both rows: d0
+                        float2* side = q_side(v, u);
+                        side[y1] = q4_minus(o, om, wd.z);
+                        side[y2] = q4_minus(om, o, wm.z);
+                    }
+                }
 #pragma unroll
                 for (int p = 0; p < 3; ++p) {
                     g[2 * p][r] = qa.q[p];
                     mir[p][r] = qb.q[p];
-                }
-                if (y1 == 0) mir[2][r] = q4_full(o, om);
-                if (r == 0 && j0) {  // texel nx = 0 of both rows: d0
-                    float2* side = q_side(v, u);
-                    side[y1] = q4_minus(o, om, wd.z);
-                    side[y2] = q4_minus(om, o, wm.z);
                 }
             }
             unmirror(mir[0], g[1]);
@@ -258,14 +282,19 @@ __global__ __launch_bounds__(N / 4) void k_pass_a3q(DevView v, float time, int t
         for (int r = 0; r < R0; ++r) {
             const float4 wd = wave_data(j + r * NJ, y, N, wb, v.gravity);
             const float2 hh = evolve_h(h[r], evolve_phase(wd.w, time));
-            const float4 wm = make_float4((j0 && r == 0) ? wd.x : -wd.x, wd.y, y ? -wd.z : wd.z, wd.w);
-            const Planes4 o = planes_of(hh, wd), om = planes_of(make_float2(hh.x, -hh.y), wm);
             QTex qa, qb;
-            q_planes(o, om, qa, qb);
+            in[3 * R0 + r] = make_float2(0.0f, 0.0f);
+            if (y != 0 && !(r == 0 && j0)) {
+                q_fast(hh, wd, qa, qb);
+            } else {  // Nyquist lines (see pass AQ)
+                const float4 wm = make_float4((j0 && r == 0) ? wd.x : -wd.x, wd.y, y ? -wd.z : wd.z, wd.w);
+                const Planes4 o = planes_of(hh, wd), om = planes_of(make_float2(hh.x, -hh.y), wm);
+                q_planes(o, om, qa, qb);
+                if (y == 0) in[3 * R0 + r] = q4_full(o, om);
+                if (r == 0 && j0) q_side(v, u)[y] = q4_minus(o, om, wd.z);
+            }
 #pragma unroll
             for (int p = 0; p < 3; ++p) in[p * R0 + r] = qa.q[p];
-            in[3 * R0 + r] = y ? make_float2(0.0f, 0.0f) : q4_full(o, om);
-            if (r == 0 && j0) q_side(v, u)[y] = q4_minus(o, om, wd.z);
         }
         const int next = item + gridDim.x;
         auto emit = [&](int m, int q, float2 val) {
