@@ -27,6 +27,14 @@ __global__ void k_write(f32x4* __restrict__ out, size_t n4, float s) {
     }
 }
 
+// write-through (sc1) float4 stores
+__global__ void k_write_sc1(f32x4* __restrict__ out, size_t n4, float s) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+        const f32x4 v = {s, s + 1.0f, s + 2.0f, (float)i};
+        asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(out + i), "v"(v) : "memory");
+    }
+}
+
 __global__ void k_read(const f32x4* __restrict__ in, size_t n4, float* sink) {
     f32x4 acc = {0, 0, 0, 0};
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x)
@@ -55,9 +63,33 @@ int main() {
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
     const int reps = 50;
-    for (int grid : {1024, 2048, 4096}) {
-        for (int mode = 0; mode < 4; ++mode) {
+    {  // beyond the Infinity Cache: 1 GiB written per launch, plain / nontemporal / write-through
+        const size_t big = (size_t)1 << 30;
+        f32x4* o2;
+        CK(hipMalloc(&o2, big));
+        for (int mode = 0; mode < 3; ++mode) {
             auto run = [&]() {
+                if (mode == 0) hipLaunchKernelGGL(k_write<false>, dim3(4096), dim3(256), 0, 0, o2, big / 16, 1.0f);
+                if (mode == 1) hipLaunchKernelGGL(k_write<true>, dim3(4096), dim3(256), 0, 0, o2, big / 16, 1.0f);
+                if (mode == 2) hipLaunchKernelGGL(k_write_sc1, dim3(4096), dim3(256), 0, 0, o2, big / 16, 1.0f);
+            };
+            for (int w = 0; w < 3; ++w) run();
+            CK(hipDeviceSynchronize());
+            CK(hipEventRecord(a));
+            for (int r = 0; r < 10; ++r) run();
+            CK(hipEventRecord(b));
+            CK(hipEventSynchronize(b));
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, a, b));
+            const char* names[] = {"write plain 1 GiB", "write nt 1 GiB", "write sc1 1 GiB"};
+            printf("%-24s grid  4096 %8.1f us %8.1f GB/s\n", names[mode], ms * 1e2, (double)big / (ms * 1e2) / 1e3);
+        }
+        CK(hipFree(o2));
+    }
+    for (int grid : {2048}) {
+        for (int mode = 0; mode < 5; ++mode) {
+            auto run = [&]() {
+                if (mode == 4) hipLaunchKernelGGL(k_write_sc1, dim3(grid), dim3(256), 0, 0, out, out_bytes / 16, 1.0f);
                 if (mode == 0) hipLaunchKernelGGL(k_write<true>, dim3(grid), dim3(256), 0, 0, out, out_bytes / 16, 1.0f);
                 if (mode == 1) hipLaunchKernelGGL(k_write<false>, dim3(grid), dim3(256), 0, 0, out, out_bytes / 16, 1.0f);
                 if (mode == 2) hipLaunchKernelGGL(k_read, dim3(grid), dim3(256), 0, 0, in, in_bytes / 16, sink);
@@ -73,7 +105,8 @@ int main() {
             CK(hipEventElapsedTime(&ms, a, b));
             const double us = ms * 1e3 / reps;
             const double bytes = mode == 2 ? in_bytes : (mode == 3 ? in_bytes + out_bytes : out_bytes);
-            const char* names[] = {"write nt 192 MiB", "write plain 192 MiB", "re-read 96 MiB", "read 96 + write nt 192"};
+            const char* names[] = {"write nt 192 MiB", "write plain 192 MiB", "re-read 96 MiB", "read 96 + write nt 192",
+                                   "write sc1 192 MiB"};
             printf("%-24s grid %5d %8.1f us %8.1f GB/s\n", names[mode], grid, us, bytes / us / 1e3);
         }
     }
