@@ -107,6 +107,29 @@ def rocprof_kernel_us(csv_name, kernel_substr, profiles_dir=os.path.join(ROOT, "
     return best
 
 
+def write_ceilings(profiles_dir=os.path.join(ROOT, "profiles")):
+    """Measured store-bandwidth ceilings of this chip from the newest committed tools/wrbench.hip run
+    (profiles/<round>/wrbench.txt): GB/s of nontemporal float4 stores over 192 MiB (pass B's texture
+    bytes) and beyond the Infinity Cache (1 GiB).  None if absent."""
+    import re
+    best = None
+    if not os.path.isdir(profiles_dir):
+        return None
+    for d in sorted(os.listdir(profiles_dir)):
+        f = os.path.join(profiles_dir, d, "wrbench.txt")
+        if not os.path.exists(f):
+            continue
+        got = {}
+        for line in open(f):
+            m = re.match(r"(write \w+ (?:192 MiB|1 GiB))\s+grid\s+\d+\s+[\d.]+ us\s+([\d.]+) GB/s", line)
+            if m:
+                got[m.group(1)] = float(m.group(2))
+        if "write nt 192 MiB" in got:
+            best = {"nt_192MiB_GBs": got["write nt 192 MiB"], "nt_beyond_cache_GBs": got.get("write nt 1 GiB"),
+                    "source": f"profiles/{d}/wrbench.txt"}
+    return best
+
+
 def beyond_cache(steps=20):
     """The frame on a working set far beyond the 256 MiB Infinity Cache: cfg4's per-GPU shard at
     8 GPUs (32 tiles x 4 x 512^2, 128 units, ~1.2 GiB of per-frame data and a 1 GiB re-read set),
@@ -337,7 +360,7 @@ def main():
         stage_us = 1e6 * (s1 - s0) / reps
         kern_us = 1e3 * (r_ms + c_ms) / reps
         rp_r = rocprof_kernel_us("ifft_kernel_stats.csv", f"k_rows2<{n},")
-        rp_c = rocprof_kernel_us("ifft_kernel_stats.csv", f"k_cols2<{n}>")
+        rp_c = rocprof_kernel_us("ifft_kernel_stats.csv", f"k_cols2<{n}")
         rocprof = None
         if rp_r and rp_c and args.config == "cfg3":
             rus = rp_r[0] + rp_c[0]
@@ -355,6 +378,15 @@ def main():
     traffic = pmc_traffic(("k_pass_b" if dom == "pass_b" else "k_pass_a") if not args.unfused
                           else ("k_cols" if dom == "ifft_cols" else "k_rows")) \
         if (args.config == "cfg3" and not args.unfused) else None
+    # the dominant kernel's store stream against the chip's measured store ceiling: pass B writes the
+    # textures (16 B DISP [+ 32 B DERIV, TURB] [+ 16 B NORMAL]) and the 4-B foam state per texel
+    writes = None
+    if dom == "pass_b" and ctx.planes == 4:
+        wb = ctx.n * ctx.n * ctx.C * ctx.T * (48 + 4)
+        wc = write_ceilings()
+        writes = {"bytes_per_launch": wb // max(1, round(launches_per_step)),
+                  "achieved_GBs": round(wb / (dom_us * 1e-6) / 1e9, 1), "measured_ceiling": wc,
+                  "frac_of_nt_ceiling": round(wb / (dom_us * 1e-6) / 1e9 / wc["nt_192MiB_GBs"], 4) if wc else None}
     cache = None
     if rank == 0 and world == 1 and args.config == "cfg3" and not args.no_beyond_cache:
         cache = {"resident_set_bytes": B["cache_resident"], "infinity_cache_bytes": 256 << 20,
@@ -394,7 +426,8 @@ def main():
                          "traffic": traffic[0] if traffic else None,
                          "traffic_source": f"profiles/{traffic[1]}/pmc_summary.json" if traffic else None,
                          "algorithmic_bytes_per_step": dom_bytes, "kernel_us_per_step": round(dom_us, 3),
-                         "launches_per_step": round(launches_per_step, 2)},
+                         "launches_per_step": round(launches_per_step, 2),
+                         "writes": writes},
             "kernels_us": {"pass_a" if not args.unfused else "rows": round(a_us, 3),
                            "pass_b" if not args.unfused else "cols": round(b_us, 3)},
             "frame": {"algorithmic_bytes_per_gpu": B["frame"],
