@@ -246,6 +246,72 @@ __global__ __launch_bounds__((WT ? WT : b3_w(N)) * N / kElems) void k_pass_b3(De
     }
 }
 
+// Pass B of a displacement-only frame (P = 2) with both planes at once: the workgroup's two halves
+// (T lanes each) run the column transforms of DyDxz and DxDz side by side, each on its own LDS image
+// (Engine SUB: lane = threadIdx.x % T; the halves meet at the same barriers), so an item is one
+// transform's latency chain instead of two; the halves then swap Dy through LDS and the DxDz half
+// stores DISP.  Small jobs (cfg2: one 512^2 cascade, one item per workgroup) are such chains.
+template <int N, int WT = 0>
+__global__ __launch_bounds__(2 * (WT ? WT : b3_w(N)) * N / kElems) void k_pass_b2d(DevView v, int items) {
+    using CT = ColTile<N, WT ? WT : b3_w(N)>;
+    using TW = typename CT::TW;
+    constexpr int W = CT::W;
+    using E = Engine<N, W, true, (CT::E::LDS_ELEMS != N * W), 16, TW, kElems, true>;
+    static_assert(E::LDS_ELEMS == CT::E::LDS_ELEMS, "same layout as the column-tile engine");
+    constexpr int T = CT::T;
+    constexpr int RL = CT::RL;
+    constexpr int TILE = W * N;
+    __shared__ float2 lds[2][E::LDS_ELEMS];
+    __shared__ float2 twl[TW::kLdsEntries];
+    __shared__ float keepy[kElems * T];
+    TW::load(twl, v.tw, threadIdx.x, 2 * T);
+    const float2* tws = TW::table(twl, v.tw);
+    const int half = (int)threadIdx.x / T;  // 0: DyDxz (plane 1), 1: DxDz (plane 0); whole waves
+    const int t = (int)threadIdx.x % T;
+    const int lb = t % W, lj = t / W;
+    const int toff = lj * W + lb;
+    const int voff16 = (lj * N + lb) * 16;
+    const int plane = half ? 0 : 1;
+    const int bt0 = v.x0 / W, bnt = v.nx / W;
+    auto full = [&](int item) { return (item / bnt) * CT::tiles + bt0 + item % bnt; };
+    auto load = [&](int item, float2 (&d)[kElems]) {
+        const Win w = make_win(v.tplane + (size_t)plane * v.inter_stride + (size_t)full(item) * TILE, TILE * 8);
+#pragma unroll
+        for (int i = 0; i < kElems; ++i) d[i] = bload2(w, toff * 8, CT::in_dy(i) * W * 8);
+    };
+    float2 cur[kElems], nxt[kElems], kxz[kElems];
+    int item = blockIdx.x;
+    if (item < items) load(item, cur);
+    __syncthreads();
+    for (; item < items; item += gridDim.x) {
+        if (item + (int)gridDim.x < items) load(item + gridDim.x, nxt);
+        const int ft = full(item);
+        const int u = ft / CT::tiles, x0 = (ft % CT::tiles) * W;
+        auto emit = [&](int m, int q, float2 val) {
+            const int i = m * RL + q;
+            const float s = perm_sign(x0 + lb, lj + CT::out_dy(m, q));
+            if (half == 0) keepy[i * T + t] = val.x * s;          // Dy
+            else kxz[i] = make_float2(val.x * s, val.y * s);      // Dx, Dz
+        };
+        E::run_regs(cur, lds[half], tws, emit);
+        __syncthreads();
+        if (half == 1) {  // DISP = (Dx, Dy, Dz, 1), streamed
+            const Win wd = make_win(v.disp + (size_t)u * N * N + x0, (unsigned)((N * N - x0) * 16));
+#pragma unroll
+            for (int m = 0; m < kElems / RL; ++m)
+#pragma unroll
+                for (int q = 0; q < RL; ++q) {
+                    const int i = m * RL + q;
+                    gstore4_nt(make_float4(kxz[i].x, keepy[i * T + t], kxz[i].y, 1.0f), wd, voff16,
+                               CT::out_dy(m, q) * N * 16);
+                }
+        }
+#pragma unroll
+        for (int i = 0; i < kElems; ++i) cur[i] = nxt[i];
+        __syncthreads();
+    }
+}
+
 // Pass A over mirror pairs (N = 1024, P = 4; DESIGN.md "pass A4").  Item i of
 // unit u covers rows y1 = i and y2 = N - i for 0 < i < N/2; item 0 covers rows
 // 0 and N/2, which are their own mirrors and are evolved texel by texel.  The
@@ -468,9 +534,26 @@ hipError_t go_b3k(const DevView& v, hipStream_t s) {
     return hipGetLastError();
 }
 
-// Two planes in flight at N = 1024 (one workgroup per CU, registers to spare).
+// narrow (4-column) tiles only: two images of a wide tile exceed the CU's LDS
+template <int N>
+hipError_t go_b2d(const DevView& v, hipStream_t s) {
+    constexpr int W = 4;
+    constexpr int T = 2 * W * N / kElems;
+    const int items = v.units * (v.nx / W);
+    const int g = grid3(k_pass_b2d<N, W>, T, items);
+    launch((k_pass_b2d<N, W>), dim3(g), dim3(T), 0, s, v, items);
+    return hipGetLastError();
+}
+
+// Two planes in flight at N = 1024 (one workgroup per CU, registers to spare).  Displacement-only
+// frames (P = 2) on narrow tiles (small jobs at N = 128..512) run both planes side by side
+// (k_pass_b2d; OCEAN_B2D=0: one after the other).
 template <int N, int P>
 hipError_t go_b3(const DevView& v, hipStream_t s) {
+    if constexpr (P == 2 && N >= 128 && N <= 512) {
+        static const int b2d = env_int("OCEAN_B2D", 1);
+        if (b2d && v.tile_w == 4) return go_b2d<N>(v, s);
+    }
     if constexpr (N == 1024) return go_b3k<N, P, 2>(v, s);
     return go_b3k<N, P, 1>(v, s);
 }

@@ -190,10 +190,15 @@ using StageTwLds = std::conditional_t<StageTw<N, R0>::kInLds, StageTw<N, R0>, St
 // butterfly j) is b-fastest (SEQ_FAST, column tiles) or j-fastest (rows).
 // Stage-0 input slot m*R0 + r is element y = j_m + r*N/R0 of sequence b_m;
 // last-stage output slot (m, q) is element y = j_m + q*N/RL.
-template <int N, int B, bool SEQ_FAST, bool PAD, int FIRST = 16, class TWT = StageTw<N, FIRST>, int EL = kElems>
+// SUB: the workgroup runs several engines side by side, THREADS lanes each (a power of two); a lane
+// works in engine threadIdx.x / THREADS as lane threadIdx.x % THREADS.
+template <int N, int B, bool SEQ_FAST, bool PAD, int FIRST = 16, class TWT = StageTw<N, FIRST>, int EL = kElems,
+          bool SUB = false>
 struct Engine {
     static constexpr int ELEMS = EL;  // complex values per lane per stage (16, or 32 for two butterflies of 16)
     static constexpr int THREADS = B * N / EL;
+    static_assert(!SUB || (THREADS & (THREADS - 1)) == 0, "side-by-side engines need a power-of-two lane count");
+    static __device__ __forceinline__ int lane() { return SUB ? (int)(threadIdx.x & (THREADS - 1)) : (int)threadIdx.x; }
     static constexpr int S = n_stages(N, FIRST);
     static constexpr int R0 = radix_of(N, 0, FIRST);
     static constexpr int RL = radix_of(N, S - 1, FIRST);
@@ -268,7 +273,7 @@ struct Engine {
 #pragma unroll
         for (int m = 0; m < BF; ++m) {
             int b, j;
-            bj<R>((int)threadIdx.x + m * THREADS, b, j);
+            bj<R>(lane() + m * THREADS, b, j);
             if constexpr (linear()) {
                 const float2* src = lds + lidx(b, j);
 #pragma unroll
@@ -282,7 +287,7 @@ struct Engine {
 #pragma unroll
         for (int m = 0; m < BF; ++m) {
             int b, j;
-            bj<R>((int)threadIdx.x + m * THREADS, b, j);
+            bj<R>(lane() + m * THREADS, b, j);
             TWT::template apply<ST>(&v[m * R], j, tws);
             Idft<R>::run(&v[m * R]);
             if constexpr (LAST) {
@@ -309,7 +314,7 @@ struct Engine {
     // Stage-0 outputs of butterfly m to LDS (Ns = 1: y = R0 j + q).
     static __device__ __forceinline__ void stage0_store(float2* lds, int m, const float2* v) {
         int b, j;
-        bj<R0>((int)threadIdx.x + m * THREADS, b, j);
+        bj<R0>(lane() + m * THREADS, b, j);
         if constexpr (linear()) {
             float2* dst = lds + lidx(b, j * R0);
 #pragma unroll
