@@ -328,9 +328,11 @@ __global__ __launch_bounds__(2 * (WT ? WT : b3_w(N)) * N / kElems) void k_pass_b
 // p0, p0 + 1 of both rows) and runs the stages twice per item: 43.5 KiB of LDS instead of
 // 78 KiB, so 3 workgroups share a CU instead of 2 and the per-workgroup latency chain
 // (evolve -> LDS stages -> stores) overlaps better: 38.6 -> 33.0 us at cfg3.
-template <int N, bool NOSTORE = false, bool BAND = false, int PH = 2, int WT = 0>
+//
+// P = 2 (displacement-only frames, N = 256 and 512): both planes in one LDS pass.
+template <int N, bool NOSTORE = false, bool BAND = false, int PH = 2, int WT = 0, int P = 4>
 __global__ __launch_bounds__(N / 4) void k_pass_a4(DevView v, float time, int items_per_unit, int items) {
-    constexpr int P = 4, R0 = 4, RB = 2, EL = 32;
+    constexpr int R0 = 4, RB = 2, EL = 2 * P * R0;
     static_assert(PH == 2 || PH == 4, "stages need 16 values per lane");
     using TW = StageTw<N, R0>;
     using E = Engine<N, RB * PH, false, true, R0, TW, EL * PH / P>;
@@ -558,26 +560,28 @@ hipError_t go_b3(const DevView& v, hipStream_t s) {
     return go_b3k<N, P, 1>(v, s);
 }
 
-template <int N, bool NOSTORE = false, bool BAND = false, int PH = 2, int WT = 0>
+template <int N, bool NOSTORE = false, bool BAND = false, int PH = 2, int WT = 0, int P = 4>
 hipError_t go_a4(const DevView& v, float t, hipStream_t s) {
     if constexpr (WT == 0) {
-        if (v.tile_w != inter_w(N)) return go_a4<N, NOSTORE, BAND, PH, 4>(v, t, s);
+        if (v.tile_w != inter_w(N)) return go_a4<N, NOSTORE, BAND, PH, 4, P>(v, t, s);
     }
     if constexpr (!BAND && !NOSTORE) {
-        if (v.nx != N) return go_a4<N, false, true, PH, WT>(v, t, s);
+        if (v.nx != N) return go_a4<N, false, true, PH, WT, P>(v, t, s);
     }
     constexpr int T = N / 4;
     const int ipu = N / 2;
     const int items = v.units * ipu;
-    const int g = grid3(k_pass_a4<N, NOSTORE, BAND, PH, WT>, T, items);
-    launch((k_pass_a4<N, NOSTORE, BAND, PH, WT>), dim3(g), dim3(T), 0, s, v, t, ipu, items);
+    const int g = grid3(k_pass_a4<N, NOSTORE, BAND, PH, WT, P>, T, items);
+    launch((k_pass_a4<N, NOSTORE, BAND, PH, WT, P>), dim3(g), dim3(T), 0, s, v, t, ipu, items);
     return hipGetLastError();
 }
 
 }  // namespace
 
 bool pass_a4_supported(int n, int planes) {
-    static const int on = env_int("OCEAN_A4_SIZES", 3);  // bit 0: N = 1024, bit 1: N = 512
+    // bit 0: N = 1024, bit 1: N = 512 (4 planes); bit 2: N = 256 / 512 (2 planes)
+    static const int on = env_int("OCEAN_A4_SIZES", 7);
+    if (planes == 2) return (on & 4) && (n == 256 || n == 512);
     return planes == 4 && ((n == 1024 && (on & 1)) || (n == 512 && (on & 2)));
 }
 
@@ -585,6 +589,10 @@ hipError_t launch_pass_a_v4(const DevView& v, float t, hipStream_t s) {
     if (!pass_a4_supported(v.n, v.planes) || !v.h0k) return hipErrorInvalidValue;
     static const int nostore = env_int("OCEAN_A4_NOSTORE", 0);
     static const int whole = env_int("OCEAN_A4_WHOLE", 0);  // 1: all 4 planes in one LDS pass (A/B)
+    if (v.planes == 2) {
+        if (v.n == 256) return go_a4<256, false, false, 2, 0, 2>(v, t, s);
+        return go_a4<512, false, false, 2, 0, 2>(v, t, s);
+    }
     if (v.n == 512) {
         if (whole) return go_a4<512, false, false, 4>(v, t, s);
         return nostore ? go_a4<512, true>(v, t, s) : go_a4<512>(v, t, s);
