@@ -690,22 +690,25 @@ def test_chunked_frame_equals_whole_frame():
 
 
 # ------------------------------------------------- cascade subsets + column bands
-@pytest.mark.parametrize("n,ncasc,world", [(256, 2, 4), (512, 4, 8), (1024, 4, 8), (4096, 2, 4), (4096, 4, 8)])
-def test_split_ocean_shards_bit_identical(n, ncasc, world):
+@pytest.mark.parametrize("n,ncasc,world,flags", [(256, 2, 4, 0), (512, 4, 8, 0), (1024, 4, 8, 0), (4096, 2, 4, 0),
+                                                 (4096, 4, 8, 0), (512, 1, 4, oh.F_DISPLACEMENT_ONLY),
+                                                 (256, 1, 2, oh.F_DISPLACEMENT_ONLY)])
+def test_split_ocean_shards_bit_identical(n, ncasc, world, flags):
     """One ocean split over `world` GPUs by ocean_hip.shard.plan_shard (cascade blocks,
     then column bands: cfg5's 8-GPU split at world = 2 x cascades), each shard its own
     context here on one GPU: every texel of every shard equals the whole ocean's bit for
     bit (the same arithmetic per texel; no data exchange), and columns outside a shard's
     band stay untouched (zero).  N = 512 / 1024 run the mirror-pair row pass, 4096 the
     four-step column passes; (4096, 4, 8) is cfg5's real 8-GPU plan (one cascade, half the
-    columns per rank)."""
+    columns per rank); the displacement-only cases (cfg2's shape) run the two-plane mirror-pair
+    row pass and the side-by-side column pass on narrow bands."""
     from ocean_hip.shard import plan_shard
     cas = O.SCENE_CASCADES[:ncasc]
-    whole, _ = make_ctx(n, cas)
+    whole, _ = make_ctx(n, cas, flags=flags)
     shards = []
     for r in range(world):
         sh = plan_shard(1, ncasc, n, world, r)
-        ctx, _ = make_ctx(n, cas[sh.casc0:sh.casc0 + sh.cascades])
+        ctx, _ = make_ctx(n, cas[sh.casc0:sh.casc0 + sh.cascades], flags=flags)
         ctx.set_column_band(sh.x0, sh.nx)
         shards.append((sh, ctx))
     assert any(sh.nx < n for sh, _ in shards)
@@ -713,7 +716,7 @@ def test_split_ocean_shards_bit_identical(n, ncasc, world):
         whole.step(t)
         for _, ctx in shards:
             ctx.step(t)
-    for tex in (oh.TEX_DISP, oh.TEX_DERIV, oh.TEX_TURB):
+    for tex in ((oh.TEX_DISP,) if flags else (oh.TEX_DISP, oh.TEX_DERIV, oh.TEX_TURB)):
         ref = whole.read_all(tex)
         for sh, ctx in shards:
             got = ctx.read_all(tex)
