@@ -290,12 +290,13 @@ bool pass_c4_supported(int n) { return n == 2048 || n == 4096; }
 
 hipError_t launch_pass_c4q(const DevView& v, hipStream_t s) {
     if (v.planes != 4 || !v.qside) return hipErrorInvalidValue;
-    hipError_t e = hipErrorInvalidValue;
-    if (v.n != 4096) return hipErrorInvalidValue;  // the three-plane frame at N >= 2048 runs at 4096 only
-    e = go_c1<4096, true>(v, s);
-    if (e != hipSuccess) return e;
-    return go_c2<4096, 4, true>(v, s);
-    return hipErrorInvalidValue;
+    if (v.n == 2048) {
+        const hipError_t e = go_c1<2048, true>(v, s);
+        return e != hipSuccess ? e : go_c2<2048, 4, true>(v, s);
+    }
+    if (v.n != 4096) return hipErrorInvalidValue;
+    const hipError_t e = go_c1<4096, true>(v, s);
+    return e != hipSuccess ? e : go_c2<4096, 4, true>(v, s);
 }
 
 hipError_t launch_pass_c4(const DevView& v, hipStream_t s) {

@@ -260,9 +260,11 @@ struct Engine {
         else __syncthreads();
     }
 
-    // Stages ST.. from LDS; the last stage hands (m, q, value) to emit.
+    // Stages ST.. from LDS; the last stage hands (m, q, value) to emit.  Butterflies of sequences
+    // b >= live are skipped (their lanes still join the stage barriers): an image with idle
+    // sequence slots.
     template <int ST, class Emit>
-    static __device__ __forceinline__ void stages_from(float2* lds, const float2* tws, Emit& emit) {
+    static __device__ __forceinline__ void stages_from(float2* lds, const float2* tws, Emit& emit, int live = B) {
         constexpr int R = radix_of(N, ST, FIRST);
         constexpr int NS = ns_of(N, ST, FIRST);
         constexpr int BF = EL / R;
@@ -274,6 +276,7 @@ struct Engine {
         for (int m = 0; m < BF; ++m) {
             int b, j;
             bj<R>(lane() + m * THREADS, b, j);
+            if (b >= live) continue;
             if constexpr (linear()) {
                 const float2* src = lds + lidx(b, j);
 #pragma unroll
@@ -288,6 +291,7 @@ struct Engine {
         for (int m = 0; m < BF; ++m) {
             int b, j;
             bj<R>(lane() + m * THREADS, b, j);
+            if (b >= live) continue;
             TWT::template apply<ST>(&v[m * R], j, tws);
             Idft<R>::run(&v[m * R]);
             if constexpr (LAST) {
@@ -307,7 +311,7 @@ struct Engine {
         }
         if constexpr (!LAST) {
             stage_sync<ST>();
-            stages_from<ST + 1>(lds, tws, emit);
+            stages_from<ST + 1>(lds, tws, emit, live);
         }
     }
 

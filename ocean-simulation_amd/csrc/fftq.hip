@@ -19,6 +19,7 @@
 // The planes Q1..Q3 (24 B / texel instead of 32) plus the per-unit side arrays d0 and srow are the
 // whole intermediate; pass B forms R[Q4] from R[Q1] on load.  The outputs equal the four-plane
 // frame's in real arithmetic, Nyquist lines included; in fp32 they differ by rounding only.
+#include <cstdlib>
 #include "fft_engine.h"
 #include "spectrum_math.h"
 
@@ -224,9 +225,9 @@ __global__ __launch_bounds__(N / 4) AQ_WPEU void k_pass_aq(DevView v, float time
                               (size_t)(jj / W) * N * W + (jj % W);
                 dst[(size_t)q * (NSL / W) * N * W] = val;
             };
-            // pass 1 at N = 1024 (wave-private stages, wave w = sequence w): waves 2, 3 idle
-            if (!(AQ_SKIP && E::wave_private(1) && ps == 1 && (int)threadIdx.x >= 128))
-                E::template stages_from<1>(lds, tws, emit);
+            // pass 1: sequence slots 2, 3 idle, their butterflies skipped (at N = 1024 the stages are
+            // wave-private, wave w = sequence w: waves 2, 3 skip them whole)
+            E::template stages_from<1>(lds, tws, emit, (AQ_SKIP && ps == 1) ? 2 : 4);
             __syncthreads();
         }
 #pragma unroll
@@ -243,7 +244,9 @@ __global__ __launch_bounds__(N / 4) AQ_WPEU void k_pass_aq(DevView v, float time
 // rows).  P(-k) is formed from the lane's own texel: h(-k) = conj h(k) bit for bit (h0.zw =
 // conj h0(-k) after ocean_init_spectrum), with the mirror's wave data (kx, kz negated except on
 // the Nyquist column / row).  16-wide tile-major intermediate as pass A3.
-template <int N, bool BAND = false>
+// S3: the LDS stages skip the idle fourth sequence slot (its butterflies' lanes only join the
+// stage barriers); row 0 runs srow's input through them in a second pass (one row in N).
+template <int N, bool BAND = false, bool S3 = true>
 __global__ __launch_bounds__(N / 4) void k_pass_a3q(DevView v, float time, int total_rows) {
     constexpr int FIRST = 4;
     using TW = StageTwLds<N, FIRST>;
@@ -297,9 +300,7 @@ __global__ __launch_bounds__(N / 4) void k_pass_a3q(DevView v, float time, int t
             for (int p = 0; p < 3; ++p) in[p * R0 + r] = qa.q[p];
         }
         const int next = item + gridDim.x;
-        auto emit = [&](int m, int q, float2 val) {
-            int b, jj;
-            E::template bj<E::RL>((int)threadIdx.x + m * T, b, jj);
+        auto put = [&](int b, int jj, int q, float2 val) {
             const int x = jj + q * NSL;
             if (b == 3) {
                 if (y == 0) q_side(v, u)[N + x] = val;  // srow
@@ -310,7 +311,35 @@ __global__ __launch_bounds__(N / 4) void k_pass_a3q(DevView v, float time, int t
             float2* dst = rowp + (size_t)(jj / W) * N * W + (jj % W);
             dst[(size_t)q * (NSL / W) * N * W] = val;
         };
-        E::run_regs(in, lds, tws, emit);
+        if constexpr (!S3) {
+            auto emit = [&](int m, int q, float2 val) {
+                int b, jj;
+                E::template bj<E::RL>((int)threadIdx.x + m * T, b, jj);
+                put(b, jj, q, val);
+            };
+            E::run_regs(in, lds, tws, emit);
+        } else {
+#pragma unroll
+            for (int p = 0; p < 4; ++p) Idft<R0>::run(&in[p * R0]);
+            // pass 0: Q1..Q3 (sequence slot 3 idle); row 0 only, pass 1: srow's input in slot 0
+            for (int ps = 0; ps < (y == 0 ? 2 : 1); ++ps) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p) {
+                    if (ps && p) continue;
+                    float2* dst = lds + E::lidx(p, j * R0);
+#pragma unroll
+                    for (int q = 0; q < R0; ++q) dst[E::loff(q, 1)] = in[(ps ? 3 : p) * R0 + q];
+                }
+                __syncthreads();
+                auto emit = [&](int m, int q, float2 val) {
+                    int b, jj;
+                    E::template bj<E::RL>((int)threadIdx.x + m * T, b, jj);
+                    put(ps ? 3 : b, jj, q, val);
+                };
+                E::template stages_from<1>(lds, tws, emit, ps ? 1 : 3);
+                if (y == 0) __syncthreads();  // LDS reused by pass 1
+            }
+        }
         __syncthreads();
         if (next < total_rows) load(next, h);
     }
@@ -471,6 +500,11 @@ int num_cus_q() {
     return cus;
 }
 
+int env_int_q(const char* name, int dflt) {
+    const char* e = std::getenv(name);
+    return e ? std::atoi(e) : dflt;
+}
+
 template <class K>
 int grid_q(K kernel, int threads, int items) {
     int per_cu = 0;
@@ -495,15 +529,19 @@ hipError_t go_aq(const DevView& v, float t, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <int N, bool BAND = false>
+template <int N, bool BAND = false, bool S3 = true>
 hipError_t go_a3q(const DevView& v, float t, hipStream_t s) {
+    if constexpr (S3) {
+        static const int s3 = env_int_q("OCEAN_A3Q_S3", 1);  // 0: the four-sequence stages on every row (A/B)
+        if (!s3) return go_a3q<N, BAND, false>(v, t, s);
+    }
     if constexpr (!BAND) {
-        if (v.nx != N) return go_a3q<N, true>(v, t, s);
+        if (v.nx != N) return go_a3q<N, true, S3>(v, t, s);
     }
     constexpr int T = N / 4;
     const int total = v.units * N;
-    const int g = grid_q(k_pass_a3q<N, BAND>, T, total);
-    launch((k_pass_a3q<N, BAND>), dim3(g), dim3(T), 0, s, v, t, total);
+    const int g = grid_q(k_pass_a3q<N, BAND, S3>, T, total);
+    launch((k_pass_a3q<N, BAND, S3>), dim3(g), dim3(T), 0, s, v, t, total);
     return hipGetLastError();
 }
 
@@ -527,13 +565,17 @@ hipError_t go_bq(const DevView& v, hipStream_t s) {
 
 // N = 2048 keeps the four-plane passes: pass A3Q's idle fourth sequence slot costs more there
 // than the column passes save (4 x 2048^2: 612 against 599 us per frame).
-bool pass_q_supported(int n, int planes) { return planes == 4 && (n == 512 || n == 1024 || n == 4096); }
+bool pass_q_supported(int n, int planes) {
+    static const int q2048 = env_int_q("OCEAN_Q2048", 0);
+    return planes == 4 && (n == 512 || n == 1024 || n == 4096 || (n == 2048 && q2048));
+}
 
 hipError_t launch_pass_a_q(const DevView& v, float t, hipStream_t s) {
     if (!pass_q_supported(v.n, v.planes) || !v.qside) return hipErrorInvalidValue;
     switch (v.n) {
         case 512: return v.h0k ? go_aq<512>(v, t, s) : hipErrorInvalidValue;
         case 1024: return v.h0k ? go_aq<1024>(v, t, s) : hipErrorInvalidValue;
+        case 2048: return go_a3q<2048>(v, t, s);
         case 4096: return go_a3q<4096>(v, t, s);
     }
     return hipErrorInvalidValue;
