@@ -42,12 +42,21 @@ __global__ void k_read(const f32x4* __restrict__ in, size_t n4, float* sink) {
     if (acc.x == 12345.0f) sink[0] = acc.y;  // keeps the loads
 }
 
-// pass BQ's mix: per 16-B read of the intermediate, 32 B of nontemporal texture stores
+// pass BQ's mix: per 16-B read of the intermediate, 32 B of nontemporal texture stores.  k_mix
+// interleaves the two stores of a lane (32-B lane stride: every store instruction writes half of
+// each line it touches); k_mix2 writes two contiguous streams (whole lines, as pass BQ's textures).
 __global__ void k_mix(const f32x4* __restrict__ in, f32x4* __restrict__ out, size_t n4in) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4in; i += (size_t)gridDim.x * blockDim.x) {
         const f32x4 v = in[i];
         __builtin_nontemporal_store(v, out + 2 * i);
         __builtin_nontemporal_store(v * 2.0f, out + 2 * i + 1);
+    }
+}
+__global__ void k_mix2(const f32x4* __restrict__ in, f32x4* __restrict__ out, size_t n4in) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4in; i += (size_t)gridDim.x * blockDim.x) {
+        const f32x4 v = in[i];
+        __builtin_nontemporal_store(v, out + i);
+        __builtin_nontemporal_store(v * 2.0f, out + n4in + i);
     }
 }
 
@@ -87,13 +96,14 @@ int main() {
         CK(hipFree(o2));
     }
     for (int grid : {2048}) {
-        for (int mode = 0; mode < 5; ++mode) {
+        for (int mode = 0; mode < 6; ++mode) {
             auto run = [&]() {
                 if (mode == 4) hipLaunchKernelGGL(k_write_sc1, dim3(grid), dim3(256), 0, 0, out, out_bytes / 16, 1.0f);
                 if (mode == 0) hipLaunchKernelGGL(k_write<true>, dim3(grid), dim3(256), 0, 0, out, out_bytes / 16, 1.0f);
                 if (mode == 1) hipLaunchKernelGGL(k_write<false>, dim3(grid), dim3(256), 0, 0, out, out_bytes / 16, 1.0f);
                 if (mode == 2) hipLaunchKernelGGL(k_read, dim3(grid), dim3(256), 0, 0, in, in_bytes / 16, sink);
                 if (mode == 3) hipLaunchKernelGGL(k_mix, dim3(grid), dim3(256), 0, 0, in, out, in_bytes / 16);
+                if (mode == 5) hipLaunchKernelGGL(k_mix2, dim3(grid), dim3(256), 0, 0, in, out, in_bytes / 16);
             };
             for (int w = 0; w < 5; ++w) run();
             CK(hipDeviceSynchronize());
@@ -104,9 +114,9 @@ int main() {
             float ms = 0;
             CK(hipEventElapsedTime(&ms, a, b));
             const double us = ms * 1e3 / reps;
-            const double bytes = mode == 2 ? in_bytes : (mode == 3 ? in_bytes + out_bytes : out_bytes);
+            const double bytes = mode == 2 ? in_bytes : ((mode == 3 || mode == 5) ? in_bytes + out_bytes : out_bytes);
             const char* names[] = {"write nt 192 MiB", "write plain 192 MiB", "re-read 96 MiB", "read 96 + write nt 192",
-                                   "write sc1 192 MiB"};
+                                   "write sc1 192 MiB", "read 96 + nt 192 lines"};
             printf("%-24s grid %5d %8.1f us %8.1f GB/s\n", names[mode], grid, us, bytes / us / 1e3);
         }
     }
