@@ -12,6 +12,7 @@
 //   4: as 0 without the foam state (72 B per texel)
 //   5: as 4 with 16-B plane loads (k_bq_mem16; its two half-line stores per lane dominate)
 //   6: as 4 as flat contiguous streams (k_flat)
+//   7: as 6 with Q1 and Q2 interleaved into one 16-byte read stream (k_flat2)
 // Build: hipcc --offload-arch=gfx950 -O3 tools/bqbench.hip -o tools/bqbench
 #include <hip/hip_runtime.h>
 
@@ -64,6 +65,19 @@ __global__ void k_flat(const float2* __restrict__ tp, size_t ps, f32x4* __restri
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
         const float2 a = tp[i], b = tp[ps + i], c = tp[2 * ps + i];
         const f32x4 v0 = {a.x, b.y, a.y, 1.0f}, v1 = {b.x, c.y, b.y, 1.0f}, v2 = {c.x, a.y, c.y, 1.0f};
+        __builtin_nontemporal_store(v0, d0 + i);
+        __builtin_nontemporal_store(v1, d1 + i);
+        __builtin_nontemporal_store(v2, d2 + i);
+    }
+}
+
+// 7: as 6 with Q1, Q2 interleaved (one 16-byte read stream) and Q3 apart (8 bytes)
+__global__ void k_flat2(const f32x4* __restrict__ q12, const float2* __restrict__ q3, f32x4* __restrict__ d0,
+                        f32x4* __restrict__ d1, f32x4* __restrict__ d2, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const f32x4 ab = q12[i];
+        const float2 c = q3[i];
+        const f32x4 v0 = {ab.x, ab.w, ab.y, 1.0f}, v1 = {ab.z, c.y, ab.w, 1.0f}, v2 = {c.x, ab.y, c.y, 1.0f};
         __builtin_nontemporal_store(v0, d0 + i);
         __builtin_nontemporal_store(v1, d1 + i);
         __builtin_nontemporal_store(v2, d2 + i);
@@ -132,7 +146,7 @@ int main() {
     const double bytes_all = (double)tex * (24 + 8 + 48);
     for (int grid : {256, 512}) {
         printf("grid %d (%d workgroups of %d lanes per CU)\n", grid, grid / 256, T);
-        for (int mode = 0; mode < 7; ++mode) {
+        for (int mode = 0; mode < 8; ++mode) {
             auto run = [&]() {
                 if (mode == 0) hipLaunchKernelGGL(k_bq_mem<0>, dim3(grid), dim3(T), 0, 0, tp, tex, foam, d0, d1, d2, items);
                 if (mode == 1) hipLaunchKernelGGL(k_bq_mem<1>, dim3(grid), dim3(T), 0, 0, tp, tex, foam, d0, d1, d2, items);
@@ -142,6 +156,9 @@ int main() {
                 if (mode == 5)
                     hipLaunchKernelGGL(k_bq_mem16, dim3(grid), dim3(T), 0, 0, (const f32x4*)tp, tex / 2, d0, d1, d2, items);
                 if (mode == 6) hipLaunchKernelGGL(k_flat, dim3(grid * 8), dim3(256), 0, 0, tp, tex, d0, d1, d2, tex);
+                if (mode == 7)
+                    hipLaunchKernelGGL(k_flat2, dim3(grid * 8), dim3(256), 0, 0, (const f32x4*)tp, tp + 2 * tex, d0, d1, d2,
+                                       tex);
             };
             for (int w = 0; w < 3; ++w) run();
             CK(hipDeviceSynchronize());
@@ -154,7 +171,8 @@ int main() {
             const double us = ms * 1e3 / 50;
             const char* names[] = {"texture layout, nt", "texture layout, plain", "tile-major outputs, nt",
                                    "texture layout, waves sweep rows", "texture layout, nt, no foam (-8 B)",
-                                   "no foam, 16-B plane loads", "no foam, flat streams (grid x 8 WGs)"};
+                                   "no foam, 16-B plane loads", "no foam, flat streams (grid x 8 WGs)",
+                                   "no foam, flat, Q1|Q2 interleaved"};
             const double bytes = mode >= 4 ? bytes_all * 72 / 80 : bytes_all;
             printf("%-34s %8.1f us %8.1f GB/s\n", names[mode], us, bytes / us / 1e3);
         }
