@@ -246,7 +246,7 @@ __global__ __launch_bounds__(N / 4) AQ_WPEU void k_pass_aq(DevView v, float time
 // the Nyquist column / row).  16-wide tile-major intermediate as pass A3.
 // S3: the LDS stages skip the idle fourth sequence slot (its butterflies' lanes only join the
 // stage barriers); row 0 runs srow's input through them in a second pass (one row in N).
-template <int N, bool BAND = false, bool S3 = true>
+template <int N, bool BAND = false, bool S3 = true, bool EARLY_PF = true>
 __global__ __launch_bounds__(N / 4) void k_pass_a3q(DevView v, float time, int total_rows) {
     constexpr int FIRST = 4;
     using TW = StageTwLds<N, FIRST>;
@@ -300,6 +300,8 @@ __global__ __launch_bounds__(N / 4) void k_pass_a3q(DevView v, float time, int t
             for (int p = 0; p < 3; ++p) in[p * R0 + r] = qa.q[p];
         }
         const int next = item + gridDim.x;
+        // the next row's h0 in flight across this row's stages (EARLY_PF; else after them)
+        if (EARLY_PF && next < total_rows) load(next, h);
         auto put = [&](int b, int jj, int q, float2 val) {
             const int x = jj + q * NSL;
             if (b == 3) {
@@ -341,7 +343,7 @@ __global__ __launch_bounds__(N / 4) void k_pass_a3q(DevView v, float time, int t
             }
         }
         __syncthreads();
-        if (next < total_rows) load(next, h);
+        if (!EARLY_PF && next < total_rows) load(next, h);
     }
 }
 
@@ -529,19 +531,21 @@ hipError_t go_aq(const DevView& v, float t, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <int N, bool BAND = false, bool S3 = true>
+template <int N, bool BAND = false, bool S3 = true, bool PF = true>
 hipError_t go_a3q(const DevView& v, float t, hipStream_t s) {
-    if constexpr (S3) {
+    if constexpr (S3 && PF) {
         static const int s3 = env_int_q("OCEAN_A3Q_S3", 1);  // 0: the four-sequence stages on every row (A/B)
-        if (!s3) return go_a3q<N, BAND, false>(v, t, s);
+        static const int pf = env_int_q("OCEAN_A3Q_PF", 1);  // 0: next row's h0 loaded after the stages (A/B)
+        if (!s3) return go_a3q<N, BAND, false, PF>(v, t, s);
+        if (!pf) return go_a3q<N, BAND, S3, false>(v, t, s);
     }
     if constexpr (!BAND) {
-        if (v.nx != N) return go_a3q<N, true, S3>(v, t, s);
+        if (v.nx != N) return go_a3q<N, true, S3, PF>(v, t, s);
     }
     constexpr int T = N / 4;
     const int total = v.units * N;
-    const int g = grid_q(k_pass_a3q<N, BAND, S3>, T, total);
-    launch((k_pass_a3q<N, BAND, S3>), dim3(g), dim3(T), 0, s, v, t, total);
+    const int g = grid_q(k_pass_a3q<N, BAND, S3, PF>, T, total);
+    launch((k_pass_a3q<N, BAND, S3, PF>), dim3(g), dim3(T), 0, s, v, t, total);
     return hipGetLastError();
 }
 
