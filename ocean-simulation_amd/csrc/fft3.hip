@@ -37,8 +37,10 @@ constexpr int pa3_rows(int N, int RS = 2) { return N >= 1024 * RS ? 1 : 1024 * R
 // this item's stores in the in-order vmcnt queue, so waiting for them never
 // waits for the stores); NOSTORE: timing experiment only (no output); BAND: a
 // column band narrower than N (stores outside it skipped; a separate instance so
-// that the whole-band frame pays no per-store test).
-template <int N, int P, int RS, bool PF, bool NOSTORE = false, bool BAND = false, int WT = 0>
+// that the whole-band frame pays no per-store test).  EPF (without PF): the next item's h0 is
+// loaded into h as soon as the evolve has read it, in flight across the stages (+16-19 VGPRs:
+// N = 4096 only, where the workgroup's occupancy does not change); else after the stages.
+template <int N, int P, int RS, bool PF, bool NOSTORE = false, bool BAND = false, int WT = 0, bool EPF = false>
 __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems) void k_pass_a3(DevView v, float time, int total_rows) {
     constexpr int RB = pa3_rows(N, RS);
     constexpr int FIRST = 16 / P;
@@ -92,6 +94,9 @@ __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems) void k_pass_a3(De
 #pragma unroll
             for (int m = 0; m < P; ++m) in[m * R0 + r] = o.p[m];
         }
+        if constexpr (!PF && EPF) {
+            if (next < items) load(next, h);
+        }
         // outputs: sequence b = p*RB + rr', element x -> tplane[p][u'][x/W][y'][x%W]
         auto emit = [&](int m, int q, float2 val) {
             if constexpr (NOSTORE) {
@@ -122,7 +127,7 @@ __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems) void k_pass_a3(De
             for (int r = 0; r < R0; ++r) h[r] = hn[r];
         }
         __syncthreads();
-        if constexpr (!PF) {
+        if constexpr (!PF && !EPF) {
             if (next < items) load(next, h);
         }
     }
@@ -507,8 +512,15 @@ hipError_t go_a3k(const DevView& v, float t, hipStream_t s) {
     constexpr int T = RB * P * N / kElems;
     const int total = v.units * N;
     const int items = (total + RB - 1) / RB;
-    const int g = grid3(k_pass_a3<N, P, RS, PF, NOSTORE, BAND, WT>, T, items);
-    launch((k_pass_a3<N, P, RS, PF, NOSTORE, BAND, WT>), dim3(g), dim3(T), 0, s, v, t, total);
+    constexpr bool EPF = (N == 4096);
+    static const int epf = env_int("OCEAN_A3_EPF", 1);  // 0: N = 4096 loads the next row after the stages (A/B)
+    if (EPF && !epf) {
+        const int g = grid3(k_pass_a3<N, P, RS, PF, NOSTORE, BAND, WT, false>, T, items);
+        launch((k_pass_a3<N, P, RS, PF, NOSTORE, BAND, WT, false>), dim3(g), dim3(T), 0, s, v, t, total);
+        return hipGetLastError();
+    }
+    const int g = grid3(k_pass_a3<N, P, RS, PF, NOSTORE, BAND, WT, EPF>, T, items);
+    launch((k_pass_a3<N, P, RS, PF, NOSTORE, BAND, WT, EPF>), dim3(g), dim3(T), 0, s, v, t, total);
     return hipGetLastError();
 }
 
