@@ -785,3 +785,47 @@ def test_four_step_column_bands_bit_identical(n, bands):
         np.testing.assert_array_equal(a.read_all(tex), b.read_all(tex))
     a.close()
     b.close()
+
+
+_VARIANT_SCRIPT = r"""
+import sys, numpy as np
+import ocean_hip as oh
+import oracle as O
+n, ncasc, flags, out = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
+ctx = oh.OceanContext(n, ncasc, 1, flags)
+ctx.set_params(O.scene_params(), O.SCENE_CASCADES[:ncasc])
+ctx.generate_noise(20251121)
+ctx.init_spectrum()
+for t in (0.0, 0.5, 250.0):
+    ctx.step(t)
+texs = (oh.TEX_DISP,) if flags else (oh.TEX_DISP, oh.TEX_DERIV, oh.TEX_TURB)
+np.savez(out, *[ctx.read_all(t) for t in texs])
+ctx.close()
+"""
+
+
+@pytest.mark.parametrize("var,n,ncasc,flags", [("OCEAN_B2D", 512, 1, oh.F_DISPLACEMENT_ONLY),
+                                               ("OCEAN_B2D", 256, 2, oh.F_DISPLACEMENT_ONLY),
+                                               ("OCEAN_A3Q_S3", 4096, 1, 0), ("OCEAN_A3Q_PF", 4096, 1, 0),
+                                               ("OCEAN_A3_EPF", 4096, 1, oh.F_DISPLACEMENT_ONLY)])
+def test_launch_variants_bit_identical(tmp_path, var, n, ncasc, flags):
+    """Schedule knobs read once per process at first launch (environment knobs):
+    side-by-side vs sequential pass-B planes (B2D), pass A3Q's idle-slot skip (S3) and early h0
+    prefetch (PF), pass A3's early prefetch at N = 4096 (EPF).  Each variant runs in its own
+    process; 3 frames incl. foam, every output bit equal."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env_base = dict(os.environ)
+    env_base["PYTHONPATH"] = os.pathsep.join([os.path.join(root, "ocean-simulation_amd"), os.path.join(root, "oracle"),
+                                              env_base.get("PYTHONPATH", "")])
+    res = []
+    for val in ("1", "0"):
+        out = str(tmp_path / f"{var}_{val}.npz")
+        env = dict(env_base, **{var: val})
+        subprocess.run([sys.executable, "-c", _VARIANT_SCRIPT, str(n), str(ncasc), str(flags), out], env=env,
+                       check=True, timeout=100)
+        with np.load(out) as z:
+            res.append([z[k] for k in sorted(z.files)])
+    for a, b in zip(*res):
+        np.testing.assert_array_equal(a, b)
