@@ -130,6 +130,26 @@ def write_ceilings(profiles_dir=os.path.join(ROOT, "profiles")):
     return best
 
 
+def shape_us(fname, label, profiles_dir=os.path.join(ROOT, "profiles")):
+    """Microsecond time of the line starting with `label` in the newest committed
+    profiles/<round>/<fname> (tools/aqbench.hip, tools/bqbench.hip: a pass's memory shape run
+    without its evolve / FFT work, 4 x 1024^2).  (us, source) or None."""
+    import re
+    best = None
+    if not os.path.isdir(profiles_dir):
+        return None
+    for d in sorted(os.listdir(profiles_dir)):
+        f = os.path.join(profiles_dir, d, fname)
+        if not os.path.exists(f):
+            continue
+        for line in open(f):
+            m = re.match(re.escape(label) + r"\s+([\d.]+) us", line)
+            if m:
+                best = (float(m.group(1)), f"profiles/{d}/{fname}")
+                break
+    return best
+
+
 def beyond_cache(steps=20):
     """The frame on a working set far beyond the 256 MiB Infinity Cache: cfg4's per-GPU shard at
     8 GPUs (32 tiles x 4 x 512^2, 128 units, ~1.2 GiB of per-frame data and a 1 GiB re-read set),
@@ -387,6 +407,13 @@ def main():
         writes = {"bytes_per_launch": wb // max(1, round(launches_per_step)),
                   "achieved_GBs": round(wb / (dom_us * 1e-6) / 1e9, 1), "measured_ceiling": wc,
                   "frac_of_nt_ceiling": round(wb / (dom_us * 1e-6) / 1e9 / wc["nt_192MiB_GBs"], 4) if wc else None}
+    # each pass against its own memory shape run without the evolve / FFT work (cfg3's shapes)
+    shape = None
+    if args.config == "cfg3" and not args.unfused and ctx.planes == 4 and n == 1024:
+        sa = shape_us("aqbench.txt", "AQ rows (y, N - y), half lines")
+        sb = shape_us("bqbench.txt", "texture layout, nt")
+        shape = {k: {"kernel_us": round(u, 3), "shape_us": v[0], "frac_of_shape": round(v[0] / u, 4), "source": v[1]}
+                 for k, u, v in (("pass_a", a_us, sa), ("pass_b", b_us, sb)) if v}
     cache = None
     if rank == 0 and world == 1 and args.config == "cfg3" and not args.no_beyond_cache:
         cache = {"resident_set_bytes": B["cache_resident"], "infinity_cache_bytes": 256 << 20,
@@ -427,7 +454,7 @@ def main():
                          "traffic_source": f"profiles/{traffic[1]}/pmc_summary.json" if traffic else None,
                          "algorithmic_bytes_per_step": dom_bytes, "kernel_us_per_step": round(dom_us, 3),
                          "launches_per_step": round(launches_per_step, 2),
-                         "writes": writes},
+                         "writes": writes, "memory_shape": shape},
             "kernels_us": {"pass_a" if not args.unfused else "rows": round(a_us, 3),
                            "pass_b" if not args.unfused else "cols": round(b_us, 3)},
             "frame": {"algorithmic_bytes_per_gpu": B["frame"],
