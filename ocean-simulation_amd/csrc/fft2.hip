@@ -124,23 +124,9 @@ __global__ __launch_bounds__(W_ * N / kElems) void k_cols2(float2* __restrict__ 
 }
 
 // --------------------------------------------------------------- launch
-int num_cus() {
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-            cus = 256;
-    }
-    return cus;
-}
-
 template <class K>
 int persistent_grid(K kernel, int threads, int items) {
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0) != hipSuccess || per_cu <= 0)
-        per_cu = 1;
-    const int g = num_cus() * per_cu;
+    const int g = device_cus() * resident_per_cu((const void*)kernel, threads);
     return items < g ? items : g;
 }
 

@@ -480,23 +480,9 @@ int env_int(const char* name, int dflt) {
     return e ? std::atoi(e) : dflt;
 }
 
-int num_cus3() {
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-            cus = 256;
-    }
-    return cus;
-}
-
 template <class K>
 int grid3(K kernel, int threads, int items) {
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0) != hipSuccess || per_cu <= 0)
-        per_cu = 1;
-    const int g = num_cus3() * per_cu;
+    const int g = device_cus() * resident_per_cu((const void*)kernel, threads);
     return items < g ? items : g;
 }
 

@@ -254,13 +254,9 @@ __global__ __launch_bounds__(kSeq * kL1 / kElems) void k_col4s2(DevView v, int i
 
 template <class K>
 int grid4(K kernel, int threads, int items, int max_per_cu = 0) {
-    int per_cu = 0, dev = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0) != hipSuccess || per_cu <= 0)
-        per_cu = 1;
+    int per_cu = resident_per_cu((const void*)kernel, threads);
     if (max_per_cu > 0 && per_cu > max_per_cu) per_cu = max_per_cu;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    const int g = cus * per_cu;
+    const int g = device_cus() * per_cu;
     return items < g ? items : g;
 }
 

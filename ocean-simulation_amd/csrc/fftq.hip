@@ -491,17 +491,6 @@ __global__ __launch_bounds__((WT ? WT : b3_w(N)) * N / kElems) void k_pass_bq(De
     }
 }
 
-int num_cus_q() {
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-            cus = 256;
-    }
-    return cus;
-}
-
 int env_int_q(const char* name, int dflt) {
     const char* e = std::getenv(name);
     return e ? std::atoi(e) : dflt;
@@ -509,10 +498,7 @@ int env_int_q(const char* name, int dflt) {
 
 template <class K>
 int grid_q(K kernel, int threads, int items) {
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0) != hipSuccess || per_cu <= 0)
-        per_cu = 1;
-    const int g = num_cus_q() * per_cu;
+    const int g = device_cus() * resident_per_cu((const void*)kernel, threads);
     return items < g ? items : g;
 }
 

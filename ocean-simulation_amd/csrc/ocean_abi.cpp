@@ -9,6 +9,9 @@
 #include <cstring>
 #include <new>
 #include <algorithm>
+#include <map>
+#include <mutex>
+#include <tuple>
 #include <string>
 #include <vector>
 
@@ -45,6 +48,40 @@ namespace ocean {
 LaunchEvents*& launch_events() {
     thread_local LaunchEvents* slot = nullptr;
     return slot;
+}
+
+namespace {
+std::mutex g_occ_mu;
+std::map<std::tuple<int, const void*, int>, int> g_occ;  // (device, kernel, threads) -> per CU
+std::map<int, int> g_cus;                                 // device -> CUs
+int current_device() {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    return dev;
+}
+}  // namespace
+
+int resident_per_cu(const void* kernel, int threads) {
+    const auto key = std::make_tuple(current_device(), kernel, threads);
+    std::lock_guard<std::mutex> lk(g_occ_mu);
+    auto it = g_occ.find(key);
+    if (it != g_occ.end()) return it->second;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0) != hipSuccess || per_cu <= 0)
+        per_cu = 1;
+    g_occ.emplace(key, per_cu);
+    return per_cu;
+}
+
+int device_cus() {
+    const int dev = current_device();
+    std::lock_guard<std::mutex> lk(g_occ_mu);
+    auto it = g_cus.find(dev);
+    if (it != g_cus.end()) return it->second;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    g_cus.emplace(dev, cus);
+    return cus;
 }
 }  // namespace ocean
 

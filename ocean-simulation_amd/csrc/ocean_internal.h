@@ -79,6 +79,12 @@ struct SpectrumParams {
 };
 
 // spectrum.hip
+// Resident workgroups per CU of `kernel` at `threads` lanes (hipOccupancyMaxActiveBlocksPerMultiprocessor,
+// at least 1) and the device's CU count, cached per device (and kernel): the queries cost microseconds
+// of host time, paid once instead of per launch (small jobs issue a launch every few microseconds).
+int resident_per_cu(const void* kernel, int threads);
+int device_cus();
+
 hipError_t launch_init_spectrum(const DevView& v, const SpectrumParams& p, hipStream_t s);
 hipError_t launch_conjugate(const DevView& v, hipStream_t s);
 hipError_t launch_evolve(const DevView& v, float t, hipStream_t s);
