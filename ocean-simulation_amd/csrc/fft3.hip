@@ -24,6 +24,8 @@
 // pass B 32 (planes) + 4 + 4 (foam) + 48 (DISP, DERIV, TURB) = 88.
 #include <cstdlib>
 
+#include <type_traits>
+
 #include "fft_engine.h"
 #include "spectrum_math.h"
 
@@ -475,6 +477,158 @@ __global__ __launch_bounds__(N / 4) void k_pass_a4(DevView v, float time, int it
     }
 }
 
+// Pass A8 (N = 512, two planes: small displacement-only jobs, cfg2): the
+// mirror pairs of k_pass_a4 on N/2 lanes with 8 values each.  Lane j holds texels x = j, j + N/2
+// of row y1 and their mirrors in row y2 (butterfly jm = (N/2 - j) % (N/2)), so it evolves two
+// texel pairs instead of four; the row transform runs radix 2 in registers, then radix 8, 8
+// (wave-private: wave w = sequence w) and 4 through LDS, twiddles from the base table
+// exp(2 pi i m / N).  An item then has 4 waves instead of 2 and half the per-lane chain.
+template <int N, int WT = 0>
+__global__ __launch_bounds__(N / 2) void k_pass_a8(DevView v, float time, int items_per_unit, int items) {
+    static_assert(N == 512, "plan 2 x 8 x 8 x 4");
+    constexpr int T = N / 2, NB = 4;  // LDS sequence b = p * 2 + s (plane p, row set s)
+    constexpr int W = WT ? WT : inter_w(N);
+    constexpr int TILES = N / W;
+    __shared__ float2 lds[padded(NB * N)];
+    __shared__ float2 twb[N];
+    __shared__ WaveBand band[kMaxCascades];
+    for (int i = threadIdx.x; i < N; i += T) twb[i] = v.tw[i];
+    if ((int)threadIdx.x < v.C) band[threadIdx.x] = wave_band(v.casc + threadIdx.x * 5);
+    const int j = (int)threadIdx.x;
+    const bool j0 = (j == 0);
+    const int jm = (T - j) & (T - 1);
+    const bool banded = v.nx != N;
+    auto rows_of = [&](int it, int& u, int& y1, int& y2) {
+        u = it / items_per_unit;
+        const int i = it - u * items_per_unit;
+        y1 = i;
+        y2 = i ? N - i : N / 2;
+    };
+    float2 A[2], B[2];
+    auto load_pair = [&](int it) {
+        int u, y1, y2;
+        rows_of(it, u, y1, y2);
+        const float2* r1 = v.h0k + ((size_t)u * N + y1) * N;
+        const float2* r2 = v.h0k + ((size_t)u * N + y2) * N;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            A[r] = r1[j + r * T];
+            B[r] = r2[(N - j - r * T) & (N - 1)];
+        }
+    };
+    // one Stockham stage (NS, R) over the four sequences from LDS; LAST hands (b, x, value) to emit
+    auto stage = [&](auto ns_c, auto r_c, auto last_c, auto&& emit) {
+        constexpr int NS = decltype(ns_c)::value, R = decltype(r_c)::value;
+        constexpr bool LAST = decltype(last_c)::value;
+        constexpr int NR = N / R, BF = NB * NR / T;
+        float2 x[BF][R];
+#pragma unroll
+        for (int m = 0; m < BF; ++m) {
+            const int g = j + m * T, b = g / NR, jj = g % NR;
+#pragma unroll
+            for (int r = 0; r < R; ++r) x[m][r] = lds[pad(b * N + jj + r * NR)];
+        }
+        if constexpr (NB * NR / T == 1 && NR == 64) __asm__ volatile("" ::: "memory");  // wave-private
+        else __syncthreads();
+#pragma unroll
+        for (int m = 0; m < BF; ++m) {
+            const int g = j + m * T, b = g / NR, jj = g % NR;
+            const int k = jj & (NS - 1);
+#pragma unroll
+            for (int r = 1; r < R; ++r) x[m][r] = cmul(x[m][r], twb[r * k * (N / (NS * R))]);
+            Idft<R>::run(x[m]);
+            if constexpr (LAST) {
+#pragma unroll
+                for (int q = 0; q < R; ++q) emit(b, jj + q * NS, x[m][q]);
+            } else {
+                const int y0 = (jj / NS) * NS * R + k;
+#pragma unroll
+                for (int q = 0; q < R; ++q) lds[pad(b * N + y0 + q * NS)] = x[m][q];
+            }
+        }
+    };
+    using std::integral_constant;
+    int item = blockIdx.x;
+    if (item < items) load_pair(item);
+    __syncthreads();  // twiddles, band
+    for (; item < items; item += gridDim.x) {
+        const int next = item + gridDim.x;
+        int u, y1, y2;
+        rows_of(item, u, y1, y2);
+        const WaveBand wb = band[(u + v.c0) % v.C];
+        float2 in[2][2][2];  // [row set s][plane p][texel slot r]
+        if (y1 != 0) {
+            float2 mir[2][2];
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const int x = j + r * T;
+                const float4 wd = wave_data(x, y1, N, wb, v.gravity);
+                const Phase e = evolve_phase(wd.w, time);
+                const Planes4 o = evolve_with(make_float4(A[r].x, A[r].y, B[r].x, -B[r].y), wd, e);
+                // mirror: kx -> -kx (except the Nyquist column x = 0), kz -> -kz, same 1/|k| and omega
+                const float4 wm = make_float4((j0 && r == 0) ? wd.x : -wd.x, wd.y, -wd.z, wd.w);
+                const Planes4 om = evolve_with(make_float4(B[r].x, B[r].y, A[r].x, -A[r].y), wm, e);
+#pragma unroll
+                for (int p = 0; p < 2; ++p) {
+                    in[0][p][r] = o.p[p];
+                    mir[p][r] = om.p[p];
+                }
+            }
+            // the mirror of texel j + T r is texel (N - j - T r) % N: slot 1 - r of butterfly jm
+            // (j != 0), slot r of butterfly 0 (j = 0)
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                in[1][p][0] = j0 ? mir[p][0] : mir[p][1];
+                in[1][p][1] = j0 ? mir[p][1] : mir[p][0];
+            }
+        } else {
+            // rows 0 and N/2: texels pair inside their row (1 item in N/2)
+            const float2* r1 = v.h0k + ((size_t)u * N + y1) * N;
+            const float2* r2 = v.h0k + ((size_t)u * N + y2) * N;
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const int x = j + r * T;
+                const float2 am = r1[(N - x) & (N - 1)], c = r2[x];
+                const Planes4 o1 = evolve_texel(make_float4(A[r].x, A[r].y, am.x, -am.y),
+                                                wave_data(x, y1, N, wb, v.gravity), time);
+                const Planes4 o2 = evolve_texel(make_float4(c.x, c.y, B[r].x, -B[r].y),
+                                                wave_data(x, y2, N, wb, v.gravity), time);
+#pragma unroll
+                for (int p = 0; p < 2; ++p) {
+                    in[0][p][r] = o1.p[p];
+                    in[1][p][r] = o2.p[p];
+                }
+            }
+        }
+        if (next < items) load_pair(next);  // in flight across the stages
+        // stage 0 (radix 2, NS = 1) in registers: outputs y = 2 jb + q
+        const int jb1 = (y1 != 0) ? jm : j;
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                Idft<2>::run(in[s][p]);
+                const int b = p * 2 + s, jb = s ? jb1 : j;
+                lds[pad(b * N + 2 * jb)] = in[s][p][0];
+                lds[pad(b * N + 2 * jb + 1)] = in[s][p][1];
+            }
+        __syncthreads();
+        auto none = [](int, int, float2) {};
+        stage(integral_constant<int, 2>{}, integral_constant<int, 8>{}, std::false_type{}, none);
+        stage(integral_constant<int, 16>{}, integral_constant<int, 8>{}, std::false_type{}, none);
+        __syncthreads();
+        auto emit = [&](int b, int x, float2 val) {
+            if (banded && (unsigned)(x - v.x0) >= (unsigned)v.nx) return;  // outside the column band
+            const int p = b >> 1, y = (b & 1) ? y2 : y1;
+            float2* dst = v.tplane + (size_t)p * v.inter_stride + ((size_t)u * TILES * N + y) * W +
+                          (size_t)(x / W) * N * W + (x % W);
+            *dst = val;
+        };
+        stage(integral_constant<int, 128>{}, integral_constant<int, 4>{}, std::true_type{}, emit);
+        __syncthreads();  // LDS reused by the next item
+    }
+}
+
 int env_int(const char* name, int dflt) {
     const char* e = std::getenv(name);
     return e ? std::atoi(e) : dflt;
@@ -574,6 +728,16 @@ hipError_t go_a4(const DevView& v, float t, hipStream_t s) {
     return hipGetLastError();
 }
 
+template <int N, int WT>
+hipError_t go_a8(const DevView& v, float t, hipStream_t s) {
+    constexpr int T = N / 2;
+    const int ipu = N / 2;
+    const int items = v.units * ipu;
+    const int g = grid3(k_pass_a8<N, WT>, T, items);
+    launch((k_pass_a8<N, WT>), dim3(g), dim3(T), 0, s, v, t, ipu, items);
+    return hipGetLastError();
+}
+
 }  // namespace
 
 bool pass_a4_supported(int n, int planes) {
@@ -589,6 +753,8 @@ hipError_t launch_pass_a_v4(const DevView& v, float t, hipStream_t s) {
     static const int whole = env_int("OCEAN_A4_WHOLE", 0);  // 1: all 4 planes in one LDS pass (A/B)
     if (v.planes == 2) {
         if (v.n == 256) return go_a4<256, false, false, 2, 0, 2>(v, t, s);
+        static const int a8 = env_int("OCEAN_A8", 1);  // 0: pass A4's 4-values-per-texel-pair layout at N = 512
+        if (a8) return v.tile_w == inter_w(512) ? go_a8<512, 0>(v, t, s) : go_a8<512, 4>(v, t, s);
         return go_a4<512, false, false, 2, 0, 2>(v, t, s);
     }
     if (v.n == 512) {
