@@ -319,6 +319,89 @@ __global__ __launch_bounds__(2 * (WT ? WT : b3_w(N)) * N / kElems) void k_pass_b
     }
 }
 
+// Pass B8 (N = 512, W = 4 narrow tiles, displacement only; cfg2): k_pass_b2d's two planes side by
+// side with 8 values per lane instead of 16.  Each half (N W / 8 lanes, lane = column lb, butterfly
+// lj) runs radix 8 in registers on rows lj + 64 r, then radix 8, 8 through LDS ([y][W] layout, one
+// W-row of padding every 16 rows), twiddles from the base table exp(2 pi i m / N); the halves swap
+// Dy through LDS and the DxDz half stores DISP.  Twice the lanes per item, half the per-lane chain.
+template <int N, int W>
+__global__ __launch_bounds__(2 * W * N / 8) void k_pass_b8(DevView v, int items) {
+    static_assert(N == 512, "plan 8 x 8 x 8");
+    constexpr int T = W * N / 8;  // lanes per half
+    constexpr int NR = N / 8;     // butterflies per column and stage
+    constexpr int TILE = W * N;
+    constexpr int TILES = N / W;
+    constexpr int IMG = TILE + (TILE / (16 * W)) * W;
+    __shared__ float2 lds[2][IMG];
+    __shared__ float2 twb[N];
+    __shared__ float keepy[8 * T];
+    for (int i = threadIdx.x; i < N; i += 2 * T) twb[i] = v.tw[i];
+    const int half = (int)threadIdx.x / T;  // 0: DyDxz (plane 1), 1: DxDz (plane 0); whole waves
+    const int t = (int)threadIdx.x % T;
+    const int lb = t % W, lj = t / W;
+    const int plane = half ? 0 : 1;
+    float2* img = lds[half];
+    auto li = [](int y, int b) { const int i = y * W + b; return i + (i / (16 * W)) * W; };
+    const int bt0 = v.x0 / W, bnt = v.nx / W;
+    auto full = [&](int item) { return (item / bnt) * TILES + bt0 + item % bnt; };
+    auto load = [&](int item, float2 (&d)[8]) {
+        const Win w = make_win(v.tplane + (size_t)plane * v.inter_stride + (size_t)full(item) * TILE, TILE * 8);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) d[r] = bload2(w, (lj * W + lb) * 8, r * NR * W * 8);
+    };
+    // Stockham stage (NS, 8) of butterfly lj of column lb from LDS
+    auto stage = [&](auto ns_c, float2 (&x)[8]) {
+        constexpr int NS = decltype(ns_c)::value;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) x[r] = img[li(lj + r * NR, lb)];
+        __syncthreads();
+        const int k = lj & (NS - 1);
+#pragma unroll
+        for (int r = 1; r < 8; ++r) x[r] = cmul(x[r], twb[r * k * (N / (NS * 8))]);
+        Idft<8>::run(x);
+    };
+    float2 cur[8], nxt[8], kxz[8];
+    int item = blockIdx.x;
+    if (item < items) load(item, cur);
+    __syncthreads();  // twiddles
+    for (; item < items; item += gridDim.x) {
+        if (item + (int)gridDim.x < items) load(item + gridDim.x, nxt);
+        const int ft = full(item);
+        const int u = ft / TILES, x0 = (ft % TILES) * W;
+        // stage 0 (NS = 1): outputs y = 8 lj + q
+        Idft<8>::run(cur);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) img[li(8 * lj + q, lb)] = cur[q];
+        __syncthreads();
+        float2 x[8];
+        stage(std::integral_constant<int, 8>{}, x);
+        {
+            const int y0 = (lj / 8) * 64 + (lj & 7);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) img[li(y0 + q * 8, lb)] = x[q];
+        }
+        __syncthreads();
+        stage(std::integral_constant<int, 64>{}, x);  // last: outputs y = lj + 64 q
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const float s = perm_sign(x0 + lb, lj + q * NR);
+            if (half == 0) keepy[q * T + t] = x[q].x * s;         // Dy
+            else kxz[q] = make_float2(x[q].x * s, x[q].y * s);   // Dx, Dz
+        }
+        __syncthreads();
+        if (half == 1) {  // DISP = (Dx, Dy, Dz, 1), streamed
+            const Win wd = make_win(v.disp + (size_t)u * N * N + x0, (unsigned)((N * N - x0) * 16));
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                gstore4_nt(make_float4(kxz[q].x, keepy[q * T + t], kxz[q].y, 1.0f), wd, (lj * N + lb) * 16,
+                           q * NR * N * 16);
+        }
+#pragma unroll
+        for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
+        __syncthreads();
+    }
+}
+
 // Pass A over mirror pairs (N = 1024, P = 4; DESIGN.md "pass A4").  Item i of
 // unit u covers rows y1 = i and y2 = N - i for 0 < i < N/2; item 0 covers rows
 // 0 and N/2, which are their own mirrors and are evolved texel by texel.  The
@@ -702,8 +785,22 @@ hipError_t go_b2d(const DevView& v, hipStream_t s) {
 // Two planes in flight at N = 1024 (one workgroup per CU, registers to spare).  Displacement-only
 // frames (P = 2) on narrow tiles (small jobs at N = 128..512) run both planes side by side
 // (k_pass_b2d; OCEAN_B2D=0: one after the other).
+template <int N>
+hipError_t go_b8(const DevView& v, hipStream_t s) {
+    constexpr int W = 4;
+    constexpr int T = 2 * W * N / 8;
+    const int items = v.units * (v.nx / W);
+    const int g = grid3(k_pass_b8<N, W>, T, items);
+    launch((k_pass_b8<N, W>), dim3(g), dim3(T), 0, s, v, items);
+    return hipGetLastError();
+}
+
 template <int N, int P>
 hipError_t go_b3(const DevView& v, hipStream_t s) {
+    if constexpr (P == 2 && N == 512) {
+        static const int b8 = env_int("OCEAN_B8", 0);  // 1: pass B8 (8 values per lane) on narrow tiles
+        if (b8 && v.tile_w == 4) return go_b8<N>(v, s);
+    }
     if constexpr (P == 2 && N >= 128 && N <= 512) {
         static const int b2d = env_int("OCEAN_B2D", 1);
         if (b2d && v.tile_w == 4) return go_b2d<N>(v, s);
