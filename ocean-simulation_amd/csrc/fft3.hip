@@ -782,9 +782,6 @@ hipError_t go_b2d(const DevView& v, hipStream_t s) {
     return hipGetLastError();
 }
 
-// Two planes in flight at N = 1024 (one workgroup per CU, registers to spare).  Displacement-only
-// frames (P = 2) on narrow tiles (small jobs at N = 128..512) run both planes side by side
-// (k_pass_b2d; OCEAN_B2D=0: one after the other).
 template <int N>
 hipError_t go_b8(const DevView& v, hipStream_t s) {
     constexpr int W = 4;
@@ -795,10 +792,13 @@ hipError_t go_b8(const DevView& v, hipStream_t s) {
     return hipGetLastError();
 }
 
+// Two planes in flight at N = 1024 (one workgroup per CU, registers to spare).  Displacement-only
+// frames (P = 2) on narrow tiles run both planes side by side: pass B8 at N = 512 (8 values per
+// lane; OCEAN_B8=0: k_pass_b2d), k_pass_b2d at N = 128..256 (OCEAN_B2D=0: one after the other).
 template <int N, int P>
 hipError_t go_b3(const DevView& v, hipStream_t s) {
     if constexpr (P == 2 && N == 512) {
-        static const int b8 = env_int("OCEAN_B8", 0);  // 1: pass B8 (8 values per lane) on narrow tiles
+        static const int b8 = env_int("OCEAN_B8", 1);  // 0: pass B2D (16 values per lane) on narrow tiles
         if (b8 && v.tile_w == 4) return go_b8<N>(v, s);
     }
     if constexpr (P == 2 && N >= 128 && N <= 512) {

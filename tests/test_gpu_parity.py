@@ -817,6 +817,8 @@ def test_launch_variants_bit_identical(tmp_path, var, n, ncasc, flags):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env_base = dict(os.environ)
+    if var == "OCEAN_B2D":
+        env_base["OCEAN_B8"] = "0"  # pass B8 (the N = 512 default) has no sequential form
     env_base["PYTHONPATH"] = os.pathsep.join([os.path.join(root, "ocean-simulation_amd"), os.path.join(root, "oracle"),
                                               env_base.get("PYTHONPATH", "")])
     res = []
@@ -829,3 +831,27 @@ def test_launch_variants_bit_identical(tmp_path, var, n, ncasc, flags):
             res.append([z[k] for k in sorted(z.files)])
     for a, b in zip(*res):
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("var,val,n,ncasc", [("OCEAN_B8", "0", 512, 1), ("OCEAN_B8", "0", 512, 2),
+                                             ("OCEAN_A8", "0", 512, 1)])
+def test_launch_variants_vs_oracle(tmp_path, var, val, n, ncasc):
+    """Displacement-only variants whose radix order differs from the default's (OCEAN_B8=0: pass B's
+    radix-16 engine instead of pass B8's radix 8 x 8 x 8; OCEAN_A8=0: pass A4's radix-16 engine), so they match within the fp32
+    tolerance, not bit for bit: each runs in its own process (knobs are read once per process), and its
+    3 frames are checked against the radix-2 oracle at 1e-5 norm-relative per channel and cascade."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, **{var: val})
+    env["PYTHONPATH"] = os.pathsep.join([os.path.join(root, "ocean-simulation_amd"), os.path.join(root, "oracle"),
+                                         env.get("PYTHONPATH", "")])
+    out = str(tmp_path / f"{var}_{val}.npz")
+    subprocess.run([sys.executable, "-c", _VARIANT_SCRIPT, str(n), str(ncasc), str(oh.F_DISPLACEMENT_ONLY), out],
+                   env=env, check=True, timeout=100)
+    cas = O.SCENE_CASCADES[:ncasc]
+    oc = O.OracleOcean(n, O.scene_params(), cas, O.generate_noise(n, 20251121), nplanes=2)
+    with np.load(out) as z:
+        disp = z["arr_0"]
+    ref = oc.step(250.0)[0]  # the script's last frame (t = 0, 0.5, 250); displacement has no history
+    assert_channels(disp[..., :3], ref[..., :3], what=f"{var}={val} disp")
