@@ -833,13 +833,14 @@ def test_launch_variants_bit_identical(tmp_path, var, n, ncasc, flags):
         np.testing.assert_array_equal(a, b)
 
 
-@pytest.mark.parametrize("var,val,n,ncasc", [("OCEAN_B8", "0", 512, 1), ("OCEAN_B8", "0", 512, 2),
-                                             ("OCEAN_A8", "0", 512, 1)])
-def test_launch_variants_vs_oracle(tmp_path, var, val, n, ncasc):
-    """Displacement-only variants whose radix order differs from the default's (OCEAN_B8=0: pass B's
-    radix-16 engine instead of pass B8's radix 8 x 8 x 8; OCEAN_A8=0: pass A4's radix-16 engine), so they match within the fp32
-    tolerance, not bit for bit: each runs in its own process (knobs are read once per process), and its
-    3 frames are checked against the radix-2 oracle at 1e-5 norm-relative per channel and cascade."""
+@pytest.mark.parametrize("var,val,n,ncasc,flags", [("OCEAN_B8", "0", 512, 1, oh.F_DISPLACEMENT_ONLY),
+                                                   ("OCEAN_B8", "0", 512, 2, oh.F_DISPLACEMENT_ONLY),
+                                                   ("OCEAN_A8", "0", 512, 1, oh.F_DISPLACEMENT_ONLY)])
+def test_launch_variants_vs_oracle(tmp_path, var, val, n, ncasc, flags):
+    """Variants whose radix order differs from the default's (OCEAN_B8=0: pass B's radix-16 engine
+    instead of pass B8's radix 8 x 8 x 8; OCEAN_A8=0: pass A4's radix-16 engine), so they match within the fp32 tolerance, not bit for bit: each runs
+    in its own process (knobs are read once per process), and its third frame (t = 250 s, foam over all
+    three) is checked against the radix-2 oracle at 1e-5 norm-relative per channel and cascade."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -847,11 +848,16 @@ def test_launch_variants_vs_oracle(tmp_path, var, val, n, ncasc):
     env["PYTHONPATH"] = os.pathsep.join([os.path.join(root, "ocean-simulation_amd"), os.path.join(root, "oracle"),
                                          env.get("PYTHONPATH", "")])
     out = str(tmp_path / f"{var}_{val}.npz")
-    subprocess.run([sys.executable, "-c", _VARIANT_SCRIPT, str(n), str(ncasc), str(oh.F_DISPLACEMENT_ONLY), out],
+    subprocess.run([sys.executable, "-c", _VARIANT_SCRIPT, str(n), str(ncasc), str(flags), out],
                    env=env, check=True, timeout=100)
     cas = O.SCENE_CASCADES[:ncasc]
-    oc = O.OracleOcean(n, O.scene_params(), cas, O.generate_noise(n, 20251121), nplanes=2)
+    full = not flags & oh.F_DISPLACEMENT_ONLY
+    oc = O.OracleOcean(n, O.scene_params(), cas, O.generate_noise(n, 20251121), nplanes=4 if full else 2)
+    for t in (0.0, 0.5, 250.0):  # the script's frames
+        ref = oc.step(t)
     with np.load(out) as z:
-        disp = z["arr_0"]
-    ref = oc.step(250.0)[0]  # the script's last frame (t = 0, 0.5, 250); displacement has no history
-    assert_channels(disp[..., :3], ref[..., :3], what=f"{var}={val} disp")
+        got = [z[k] for k in sorted(z.files)]
+    assert_channels(got[0][..., :3], ref[0][..., :3], what=f"{var}={val} disp")
+    if full:
+        assert_channels(got[1], ref[1], what=f"{var}={val} deriv")
+        assert_channels(got[2], ref[2], what=f"{var}={val} turb")
