@@ -838,9 +838,9 @@ def test_launch_variants_bit_identical(tmp_path, var, n, ncasc, flags):
                                                    ("OCEAN_A8", "0", 512, 1, oh.F_DISPLACEMENT_ONLY)])
 def test_launch_variants_vs_oracle(tmp_path, var, val, n, ncasc, flags):
     """Variants whose radix order differs from the default's (OCEAN_B8=0: pass B's radix-16 engine
-    instead of pass B8's radix 8 x 8 x 8; OCEAN_A8=0: pass A4's radix-16 engine), so they match within the fp32 tolerance, not bit for bit: each runs
-    in its own process (knobs are read once per process), and its third frame (t = 250 s, foam over all
-    three) is checked against the radix-2 oracle at 1e-5 norm-relative per channel and cascade."""
+    instead of pass B8's radix 8 x 8 x 8; OCEAN_A8=0: pass A4's radix-16 engine), so they match within
+    the fp32 tolerance, not bit for bit: each runs in its own process (knobs are read once per
+    process), and its third frame (t = 250 s, foam over all three) is checked against the radix-2 oracle at 1e-5 norm-relative per channel and cascade."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
