@@ -40,7 +40,16 @@
 extern "C" {
 #endif
 
-#define OCEAN_ABI_VERSION 1
+/* Version history (a host checks ocean_abi_version() at load time):
+ *   1  round-1 entry points.
+ *   2  semantics changed: ocean_set_params only stages values until ocean_init_spectrum;
+ *      ocean_init_spectrum no longer zeroes the foam (ocean_reset_foam does); ocean_write
+ *      of OCEAN_TEX_WAVES is E_UNSUPPORTED without OCEAN_F_UNFUSED; ocean_sample_world*
+ *      return E_STATE before ocean_init_spectrum and the device entry checks alignment.
+ *      New: ocean_reset_foam, ocean_set_column_band, ocean_sample_world(_device),
+ *      ocean_read_async family, ocean_host_alloc/free, ocean_generate_noise_device,
+ *      ocean_kernel_name. */
+#define OCEAN_ABI_VERSION 2
 
 /* status codes */
 #define OCEAN_OK 0
@@ -210,6 +219,12 @@ int ocean_synchronize(ocean_ctx *ctx);
 int ocean_set_kernel_timing(ocean_ctx *ctx, int enable);
 int ocean_kernel_stats(ocean_ctx *ctx, int kind, double *total_ms, long long *launches);
 
+/* Symbol (demangled, as rocprofv3 reports it) of the kernel most recently launched in `kind`
+ * (0, 1, 2 as above) by this context, NUL-terminated into buf[len].  OCEAN_E_STATE if none yet;
+ * OCEAN_E_INVALID_ARG if it does not fit.  Measurement only (no reference counterpart): lets a
+ * bench match profiler records to the exact kernel that ran. */
+int ocean_kernel_name(ocean_ctx *ctx, int kind, char *buf, size_t len);
+
 /* Algorithmic HBM bytes one ocean_step moves in the schedule this context runs
  * (the roofline numerator; no reference counterpart -- measurement only):
  * fused: *pass_a = pass A (evolve + row IFFT), *pass_b = pass B (column IFFT +
@@ -245,8 +260,9 @@ int ocean_get_mip_ptr(ocean_ctx *ctx, int texture, int level, void **ptr, size_t
  * and floor(lod) + 1 (lod clamped to [0, log2 N]) when the context has OCEAN_F_MIPS,
  * else level 0.  DISPLACEMENT_ONLY contexts return zero derivatives and turbulence.
  * ocean_sample_world takes host buffers and blocks; ocean_sample_world_device takes
- * device pointers (points 4-B aligned, out 16-B aligned) and is async on the ctx
- * stream, ordered after the queued steps.  count = 0 is a no-op. */
+ * device pointers (points 4-B aligned, out 16-B aligned, else OCEAN_E_INVALID_ARG) and
+ * is async on the ctx stream, ordered after the queued steps.  count = 0 is a no-op.
+ * Both return OCEAN_E_STATE before ocean_init_spectrum. */
 int ocean_sample_world(ocean_ctx *ctx, int tile, const float *points, int count, float *out);
 int ocean_sample_world_device(ocean_ctx *ctx, int tile, const float *points, int count, float *out);
 

@@ -91,6 +91,8 @@ namespace OceanHip
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
         public static extern OceanStatus ocean_kernel_stats(IntPtr ctx, int kind, out double totalMs, out long launches);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
+        public static extern OceanStatus ocean_kernel_name(IntPtr ctx, int kind, [Out] byte[] buf, UIntPtr len);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
         public static extern OceanStatus ocean_step_bytes(IntPtr ctx, out ulong passA, out ulong passB);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
         public static extern OceanStatus ocean_set_column_band(IntPtr ctx, int xBegin, int xCount);

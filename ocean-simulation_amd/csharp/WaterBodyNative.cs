@@ -37,6 +37,16 @@ namespace OceanHip
             ApplyParams();
             OceanNative.Check(OceanNative.ocean_generate_noise(ctx, seed), "ocean_generate_noise");
             OceanNative.Check(OceanNative.ocean_init_spectrum(ctx), "ocean_init_spectrum");
+            // readback ring: MaxReadbacksInFlight pinned slices allocated once, reused by every
+            // request and freed only in Dispose (hipHostFree synchronizes the device: a free per
+            // request would make each Update wait for the frame it just queued)
+            int bytes = texturesSize * texturesSize * 4 * sizeof(float);
+            for (int i = 0; i < MaxReadbacksInFlight; i++)
+            {
+                OceanNative.Check(OceanNative.ocean_host_alloc((UIntPtr)bytes, out var b), "ocean_host_alloc");
+                ring.Add(b);
+                idle.Push(b);
+            }
         }
 
         void ApplyParams()
@@ -66,10 +76,12 @@ namespace OceanHip
         // WaterBody.Update (:284-297): step, then issue a new asynchronous request of the
         // displacement slice 0 EVERY frame (AsyncGPUReadback.Request, :288); requests
         // complete in order and each completed one refreshes buoyancyData, as the
-        // reference's callback does (:292-295).  Each request has its own pinned buffer.
-        const int MaxReadbacksInFlight = 8;  // the reference's request queue is engine-managed
+        // reference's callback does (:292-295).  Requests land in slots of a pinned ring.
+        const int MaxReadbacksInFlight = 8;  // ring slots; the reference's request queue is engine-managed
         readonly System.Collections.Generic.Queue<(IntPtr req, IntPtr buf)> readbacks =
             new System.Collections.Generic.Queue<(IntPtr req, IntPtr buf)>();
+        readonly System.Collections.Generic.List<IntPtr> ring = new System.Collections.Generic.List<IntPtr>();
+        readonly System.Collections.Generic.Stack<IntPtr> idle = new System.Collections.Generic.Stack<IntPtr>();
 
         void Complete((IntPtr req, IntPtr buf) r, bool wait)
         {
@@ -82,7 +94,7 @@ namespace OceanHip
                 System.Runtime.InteropServices.Marshal.Copy(r.buf, buoyancyData, 0, n);
             }                                              // st < 0: request.hasError, data dropped
             OceanNative.ocean_readback_release(r.req);
-            OceanNative.ocean_host_free(r.buf);
+            idle.Push(r.buf);                              // slot back to the ring
         }
 
         public void Update(float time)
@@ -90,12 +102,12 @@ namespace OceanHip
             CalculateWavesTexturesAtTime(time);
             while (readbacks.Count > 0 && OceanNative.ocean_readback_status(readbacks.Peek().req) != 0)
                 Complete(readbacks.Dequeue(), false);
-            if (readbacks.Count >= MaxReadbacksInFlight) Complete(readbacks.Dequeue(), true);
+            if (idle.Count == 0) Complete(readbacks.Dequeue(), true);  // every slot in flight: wait for the oldest
             int n = texturesSize * texturesSize * 4;
-            OceanNative.Check(OceanNative.ocean_host_alloc((UIntPtr)(n * sizeof(float)), out var buf), "ocean_host_alloc");
+            var buf = idle.Pop();
             var st = OceanNative.ocean_read_async(ctx, OceanTexture.Displacement, 0, 0, buf,
                                                   (UIntPtr)(n * sizeof(float)), out var req);
-            if (st != OceanStatus.Ok) { OceanNative.ocean_host_free(buf); OceanNative.Check(st, "ocean_read_async"); }
+            if (st != OceanStatus.Ok) { idle.Push(buf); OceanNative.Check(st, "ocean_read_async"); }
             readbacks.Enqueue((req, buf));
         }
 
@@ -138,12 +150,10 @@ namespace OceanHip
 
         public void Dispose()
         {
-            while (readbacks.Count > 0)
-            {
-                var r = readbacks.Dequeue();
-                OceanNative.ocean_readback_release(r.req);
-                OceanNative.ocean_host_free(r.buf);
-            }
+            while (readbacks.Count > 0) OceanNative.ocean_readback_release(readbacks.Dequeue().req);
+            foreach (var b in ring) OceanNative.ocean_host_free(b);
+            ring.Clear();
+            idle.Clear();
             if (ctx != IntPtr.Zero) OceanNative.ocean_destroy(ctx);
             ctx = IntPtr.Zero;
         }

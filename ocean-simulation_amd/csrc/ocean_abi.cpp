@@ -1,6 +1,7 @@
 // C-ABI layer of liboceanhip.so: context lifetime, validation, device memory,
 // the per-frame schedule, readback and kernel timing.  See include/ocean/ocean.h
 // for the reference interface each entry point replaces.
+#include <cxxabi.h>
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -47,6 +48,10 @@ struct TimedLaunch {
 namespace ocean {
 LaunchEvents*& launch_events() {
     thread_local LaunchEvents* slot = nullptr;
+    return slot;
+}
+const void*& last_kernel() {
+    thread_local const void* slot = nullptr;
     return slot;
 }
 
@@ -141,6 +146,7 @@ struct ocean_ctx {
     std::vector<TimedLaunch> pending;
     double kind_ms[3] = {0, 0, 0};
     long long kind_count[3] = {0, 0, 0};
+    const void* kind_kernel[3] = {nullptr, nullptr, nullptr};  // last kernel launched per kind (ocean_kernel_name)
     static constexpr size_t kMaxPending = 2048;  // timed launches held before folding into kind_ms
 
     size_t texels() const { return (size_t)n * n; }
@@ -232,8 +238,10 @@ int fold_pending(ocean_ctx* ctx, bool wait) {
 // at most kMaxPending launches' events.
 template <class F>
 int timed(ocean_ctx* ctx, int kind, F&& launch, const char* what) {
+    ocean::last_kernel() = nullptr;
     if (!ctx->timing) {
         const hipError_t e = launch();
+        if (ocean::last_kernel()) ctx->kind_kernel[kind] = ocean::last_kernel();
         return e == hipSuccess ? OCEAN_OK : hip_fail(e, what);
     }
     if (ctx->pending.size() >= ocean_ctx::kMaxPending) {
@@ -246,6 +254,7 @@ int timed(ocean_ctx* ctx, int kind, F&& launch, const char* what) {
     ocean::launch_events() = &ev;  // the kernels of this entry carry the events (ocean_internal.h)
     const hipError_t e = launch();
     ocean::launch_events() = nullptr;
+    if (ocean::last_kernel()) ctx->kind_kernel[kind] = ocean::last_kernel();
     if (e != hipSuccess) return hip_fail(e, what);
     if (!ev.launched) {  // nothing was launched: an empty interval
         OCEAN_HIP(hipEventRecord(ev.start, ctx->stream));
@@ -915,11 +924,16 @@ static int check_sample(ocean_ctx* ctx, int tile, const float* pts, int count, f
     if (tile < 0 || tile >= ctx->T) return fail(OCEAN_E_INVALID_ARG, "tile out of range");
     if (count < 0) return fail(OCEAN_E_INVALID_ARG, "negative point count");
     if (count > 0 && (!pts || !out)) return fail(OCEAN_E_INVALID_ARG, "null points or output");
+    // the cascade constants (wavelengths) the sampler divides by exist only after init
+    if (!ctx->spectrum_ready) return fail(OCEAN_E_STATE, "ocean_init_spectrum must precede ocean_sample_world");
     return OCEAN_OK;
 }
 
 int ocean_sample_world_device(ocean_ctx* ctx, int tile, const float* points, int count, float* out) {
     if (int r = check_sample(ctx, tile, points, count, out)) return r;
+    // k_sample_world reads floats and writes float4 rows (ocean.h)
+    if (((uintptr_t)points & 3) || ((uintptr_t)out & 15))
+        return fail(OCEAN_E_INVALID_ARG, "ocean_sample_world_device: points must be 4-byte and out 16-byte aligned");
     const ocean::DevView v = ctx->view();
     return timed(ctx, 2, [&] { return ocean::launch_sample_world(v, tile, points, count, out, ctx->stream); },
                  "sample_world");
@@ -1009,6 +1023,22 @@ int ocean_step_bytes(ocean_ctx* ctx, uint64_t* pass_a, uint64_t* pass_b) {
     *pass_a = a;
     *pass_b = b;
     return OCEAN_OK;
+}
+
+int ocean_kernel_name(ocean_ctx* ctx, int kind, char* buf, size_t len) {
+    if (!ctx || !buf || len == 0) return fail(OCEAN_E_INVALID_ARG, "null argument or zero length");
+    if (kind < 0 || kind > 2) return fail(OCEAN_E_INVALID_ARG, "bad kind");
+    buf[0] = 0;
+    if (!ctx->kind_kernel[kind]) return fail(OCEAN_E_STATE, "no kernel of this kind launched yet");
+    if (int r = enter(ctx)) return r;
+    const char* mangled = hipKernelNameRefByPtr(ctx->kind_kernel[kind], ctx->stream);
+    if (!mangled) return fail(OCEAN_E_DEVICE, "hipKernelNameRefByPtr returned no name");
+    int st = 0;
+    char* dem = abi::__cxa_demangle(mangled, nullptr, nullptr, &st);
+    const std::string name = (st == 0 && dem) ? dem : mangled;
+    std::free(dem);
+    std::snprintf(buf, len, "%s", name.c_str());
+    return name.size() < len ? OCEAN_OK : fail(OCEAN_E_INVALID_ARG, "buffer too small for " + name);
 }
 
 int ocean_kernel_stats(ocean_ctx* ctx, int kind, double* total_ms, long long* launches) {

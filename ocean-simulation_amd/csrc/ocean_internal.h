@@ -20,9 +20,12 @@ struct LaunchEvents {
     bool launched;
 };
 LaunchEvents*& launch_events();  // thread-local slot, ocean_abi.cpp
+// Host pointer of the kernel this thread launched last (ocean_kernel_name reports its symbol).
+const void*& last_kernel();  // thread-local slot, ocean_abi.cpp
 
 template <class F, class... Args>
 inline void launch(F kernel, dim3 grid, dim3 block, uint32_t shmem, hipStream_t s, Args... args) {
+    last_kernel() = (const void*)kernel;
     LaunchEvents* e = launch_events();
     hipExtLaunchKernelGGL(kernel, grid, block, shmem, s, e && !e->launched ? e->start : nullptr,
                           e ? e->stop : nullptr, 0, args...);

@@ -37,7 +37,7 @@ public:
     std::vector<WaterCascade> cascades{WaterCascade{}};
     uint64_t seed = 20251121;  // the reference's UnityEngine.Random is unseeded; this library's generator is
     int device = 0;
-    size_t maxReadbacksInFlight = 8;  // bound on queued requests (the reference's queue is engine-managed)
+    size_t maxReadbacksInFlight = 8;  // pinned ring slots = bound on queued requests (set before Awake)
 
     WaterBody() = default;
     WaterBody(const WaterBody&) = delete;
@@ -49,6 +49,15 @@ public:
         ApplyParams();
         check(ocean_generate_noise(ctx_, seed), "ocean_generate_noise");
         check(ocean_init_spectrum(ctx_), "ocean_init_spectrum");
+        // the readback ring: maxReadbacksInFlight pinned slices allocated once and reused, freed only
+        // in OnDisable (hipHostFree synchronizes the device, so a free per request would make every
+        // Update wait for the frame it just queued)
+        for (size_t i = 0; i < std::max<size_t>(maxReadbacksInFlight, 1); ++i) {
+            void* b = nullptr;
+            check(ocean_host_alloc(SliceBytes(), &b), "ocean_host_alloc");
+            free_.push_back(b);
+            owned_.push_back(b);
+        }
     }
 
     // Parameter change -> spectrum re-init; the foam accumulator carries over, as there.
@@ -69,16 +78,16 @@ public:
             if (st == 0) break;
             Complete(st);
         }
-        if (readbacks_.size() >= maxReadbacksInFlight) {
-            check(ocean_readback_wait(readbacks_.front().req), "ocean_readback_wait");
-            Complete(1);
+        if (free_.empty()) {  // every ring slot in flight: wait for the oldest request
+            const int st = ocean_readback_wait(readbacks_.front().req) == OCEAN_OK ? 1 : -1;
+            Complete(st);
         }
         Pending p;
-        const size_t bytes = SliceBytes();
-        check(ocean_host_alloc(bytes, &p.buf), "ocean_host_alloc");
-        const int rc = ocean_read_async(ctx_, OCEAN_TEX_DISP, 0, 0, p.buf, bytes, &p.req);
+        p.buf = free_.back();
+        free_.pop_back();
+        const int rc = ocean_read_async(ctx_, OCEAN_TEX_DISP, 0, 0, p.buf, SliceBytes(), &p.req);
         if (rc != OCEAN_OK) {
-            ocean_host_free(p.buf);
+            free_.push_back(p.buf);
             check(rc, "ocean_read_async");
         }
         readbacks_.push_back(p);
@@ -120,11 +129,11 @@ public:
     }
 
     void OnDisable() {
-        for (auto& p : readbacks_) {
-            ocean_readback_release(p.req);
-            ocean_host_free(p.buf);
-        }
+        for (auto& p : readbacks_) ocean_readback_release(p.req);
         readbacks_.clear();
+        for (void* b : owned_) ocean_host_free(b);
+        owned_.clear();
+        free_.clear();
         if (ctx_) ocean_destroy(ctx_);
         ctx_ = nullptr;
     }
@@ -140,6 +149,7 @@ private:
     };
     ocean_ctx* ctx_ = nullptr;
     std::deque<Pending> readbacks_;
+    std::vector<void*> free_, owned_;  // pinned readback ring: idle slots, all slots
     std::vector<float> buoyancyData_;
     long requested_ = 0, completed_ = 0;
 
@@ -162,7 +172,7 @@ private:
             ++completed_;
         }
         ocean_readback_release(p.req);
-        ocean_host_free(p.buf);
+        free_.push_back(p.buf);  // back to the ring
     }
 };
 

@@ -61,7 +61,7 @@ EXPORTED_SYMBOLS = (
     "ocean_set_kernel_timing", "ocean_kernel_stats", "ocean_step_bytes", "ocean_read_mip", "ocean_get_mip_ptr",
     "ocean_generate_noise_device", "ocean_read_async", "ocean_readback_status", "ocean_readback_wait", "ocean_readback_release",
     "ocean_host_alloc", "ocean_host_free", "ocean_last_error", "ocean_abi_version", "ocean_set_column_band",
-    "ocean_reset_foam", "ocean_sample_world", "ocean_sample_world_device",
+    "ocean_reset_foam", "ocean_sample_world", "ocean_sample_world_device", "ocean_kernel_name",
 )
 
 
@@ -116,6 +116,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "ocean_synchronize": ([P], i),
         "ocean_set_kernel_timing": ([P, i], i),
         "ocean_kernel_stats": ([P, i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong)], i),
+        "ocean_kernel_name": ([P, i, ctypes.c_char_p, sz], i),
         "ocean_step_bytes": ([P, ctypes.POINTER(u64), ctypes.POINTER(u64)], i),
         "ocean_read_mip": ([P, i, i, i, i, P, sz], i),
         "ocean_generate_noise_device": ([P, u64], i),
@@ -258,10 +259,11 @@ class OceanContext:
                "ocean_sample_world")
         return out
 
-    def read_async(self, tex: int, tile: int = 0, cascade: int = 0) -> "Readback":
+    def read_async(self, tex: int, tile: int = 0, cascade: int = 0, buf: "PinnedBuffer" = None) -> "Readback":
         """AsyncGPUReadback.Request (WaterBody.cs:288-296): copy one slice into pinned
-        host memory once the queued steps finish; poll .done() / .wait(), then .data."""
-        return Readback(self, tex, tile, cascade)
+        host memory once the queued steps finish; poll .done() / .wait(), then .data.
+        `buf`: a caller-owned pinned slot to land in (else the request allocates its own)."""
+        return Readback(self, tex, tile, cascade, buf)
 
     def device_ptr(self, tex: int):
         p, b = ctypes.c_void_p(), ctypes.c_size_t()
@@ -287,6 +289,16 @@ class OceanContext:
         _check(self.lib.ocean_kernel_stats(self._h, kind, ctypes.byref(ms), ctypes.byref(cnt)), "ocean_kernel_stats")
         return ms.value, cnt.value
 
+    def kernel_name(self, kind: int) -> Optional[str]:
+        """Demangled symbol of the kernel this context launched last in `kind` (0 pass A / rows,
+        1 pass B / columns, 2 other), as rocprofv3 names it; None before any such launch."""
+        buf = ctypes.create_string_buffer(1024)
+        rc = self.lib.ocean_kernel_name(self._h, kind, buf, len(buf))
+        if rc == E_STATE:
+            return None
+        _check(rc, "ocean_kernel_name")
+        return buf.value.decode()
+
     def step_bytes(self):
         """(pass A, pass B) algorithmic HBM bytes of one step in this context's schedule."""
         a, b = ctypes.c_uint64(), ctypes.c_uint64()
@@ -294,20 +306,51 @@ class OceanContext:
         return a.value, b.value
 
 
-class Readback:
-    """One ocean_read_async request into pinned host memory (ocean_host_alloc)."""
+class PinnedBuffer:
+    """Pinned host memory from ocean_host_alloc, freed by release() (hipHostFree synchronizes the
+    device, so a host that reads back every frame allocates its slots once and reuses them)."""
 
-    def __init__(self, ctx: "OceanContext", tex: int, tile: int, cascade: int):
+    def __init__(self, nbytes: int):
+        self.lib = load_library()
+        self.nbytes = nbytes
+        self.ptr = ctypes.c_void_p()
+        _check(self.lib.ocean_host_alloc(nbytes, ctypes.byref(self.ptr)), "ocean_host_alloc")
+
+    def release(self) -> None:
+        if self.ptr:
+            self.lib.ocean_host_free(self.ptr)
+            self.ptr = ctypes.c_void_p()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.release()
+        except Exception:
+            pass
+
+
+class Readback:
+    """One ocean_read_async request into pinned host memory: a caller's PinnedBuffer slot, or
+    one of its own (freed by release())."""
+
+    def __init__(self, ctx: "OceanContext", tex: int, tile: int, cascade: int, buf: Optional[PinnedBuffer] = None):
         self.lib = ctx.lib
         ch = _TEX_CHANNELS[tex]
         self.shape = (ctx.n, ctx.n, ch)
         self.nbytes = ctx.n * ctx.n * ch * 4
-        self._buf = ctypes.c_void_p()
         self._h = ctypes.c_void_p()
-        _check(self.lib.ocean_host_alloc(self.nbytes, ctypes.byref(self._buf)), "ocean_host_alloc")
+        self.slot = buf
+        self._own = buf is None
+        if buf is None:
+            buf = PinnedBuffer(self.nbytes)
+        elif buf.nbytes < self.nbytes:
+            raise ValueError(f"pinned slot of {buf.nbytes} B < slice {self.nbytes} B")
+        self._pinned = buf
+        self._buf = buf.ptr
         rc = self.lib.ocean_read_async(ctx._h, tex, tile, cascade, self._buf, self.nbytes, ctypes.byref(self._h))
         if rc != OK:
-            self.lib.ocean_host_free(self._buf)
+            if self._own:
+                buf.release()
+            self._pinned = None
             self._buf = ctypes.c_void_p()
             _check(rc, "ocean_read_async")
 
@@ -331,9 +374,10 @@ class Readback:
         if self._h:
             self.lib.ocean_readback_release(self._h)
             self._h = ctypes.c_void_p()
-        if self._buf:
-            self.lib.ocean_host_free(self._buf)
-            self._buf = ctypes.c_void_p()
+        if self._pinned is not None and self._own:
+            self._pinned.release()
+        self._pinned = None
+        self._buf = ctypes.c_void_p()
 
     def __del__(self):  # pragma: no cover
         try:
@@ -390,6 +434,8 @@ class WaterBody:
         self.ctx: Optional[OceanContext] = None
         self.buoyancyData: Optional[np.ndarray] = None
         self._readbacks: List[Readback] = []
+        self._ring: List[PinnedBuffer] = []  # pinned readback slots, allocated in Awake
+        self._idle: List[PinnedBuffer] = []
 
     def params(self) -> dict:
         return dict(wind_speed=self.windSpeed, wind_dir_x=self.windDirection[0], wind_dir_y=self.windDirection[1],
@@ -408,6 +454,9 @@ class WaterBody:
         else:
             self.ctx.generate_noise(self.seed)
         self.ctx.init_spectrum()
+        slice_bytes = self.texturesSize * self.texturesSize * 16
+        self._ring = [PinnedBuffer(slice_bytes) for _ in range(self.MAX_READBACKS_IN_FLIGHT)]
+        self._idle = list(self._ring)
         return self
 
     def OnValidate(self) -> None:
@@ -419,7 +468,7 @@ class WaterBody:
     def CalculateWavesTexturesAtTime(self, time: float) -> None:
         self.ctx.step(time)
 
-    MAX_READBACKS_IN_FLIGHT = 8  # bound on queued requests (the reference's queue is engine-managed)
+    MAX_READBACKS_IN_FLIGHT = 8  # pinned ring slots = bound on queued requests (the reference's queue is engine-managed)
 
     def Update(self, time: float) -> None:
         """WaterBody.Update (WaterBody.cs:284-297): step, then issue a new AsyncGPUReadback
@@ -427,13 +476,21 @@ class WaterBody:
         each completed one refreshes buoyancyData, as the reference's callback does (:292-295)."""
         self.CalculateWavesTexturesAtTime(time)
         self._poll_readbacks()
-        if len(self._readbacks) >= self.MAX_READBACKS_IN_FLIGHT:
+        if not self._idle:  # every ring slot in flight: wait for the oldest request
             self._complete(self._readbacks.pop(0))
-        self._readbacks.append(self.ctx.read_async(TEX_DISP, 0, 0))
+        slot = self._idle.pop()
+        try:
+            self._readbacks.append(self.ctx.read_async(TEX_DISP, 0, 0, slot))
+        except Exception:
+            self._idle.append(slot)
+            raise
 
     def _complete(self, rb: "Readback") -> None:
         self.buoyancyData = rb.data
+        slot = rb.slot
         rb.release()
+        if slot is not None:
+            self._idle.append(slot)
 
     def _poll_readbacks(self) -> None:
         while self._readbacks and self._readbacks[0].done():
@@ -478,6 +535,9 @@ class WaterBody:
         for rb in self._readbacks:
             rb.release()
         self._readbacks = []
+        for b in self._ring:
+            b.release()
+        self._ring, self._idle = [], []
         if self.ctx is not None:
             self.ctx.close()
             self.ctx = None

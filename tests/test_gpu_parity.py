@@ -262,11 +262,15 @@ def test_large_time_vs_oracle(times):
     ctx.close()
 
 
-def test_cfg4_shape_chunked_tiles():
-    """cfg4's per-GPU shard (32 tiles x 4 cascades x 512^2, 128 units) at the DEFAULT unit
-    chunking (192 MiB of intermediate = 24 units per chunk: boundaries at units 24, 48, ...,
-    which fall mid-ocean at tile 6, and a partial last chunk of 8 units): every tile equals a
-    single-tile context bit for bit, and two tiles match the oracle."""
+@pytest.mark.parametrize("chunk_mib", [None, 120])
+def test_cfg4_shape_chunked_tiles(chunk_mib, monkeypatch):
+    """cfg4's per-GPU shard (32 tiles x 4 cascades x 512^2, 128 units) through the three-plane frame
+    at the default unit chunking (192 MiB of intermediate at 24 B per texel = 32 units per chunk:
+    4 whole chunks) and at OCEAN_CHUNK_MIB=120 (20 units = 5 tiles per chunk: 6 chunks and a partial
+    last chunk of 8 units, every chunk rewriting the same reused intermediate region): every tile
+    equals a single-tile context bit for bit, and two tiles match the oracle."""
+    if chunk_mib is not None:
+        monkeypatch.setenv("OCEAN_CHUNK_MIB", str(chunk_mib))
     n, cas, T, seed = 512, O.SCENE_CASCADES, 32, 20251121 + 32
     ctx = oh.OceanContext(n, 4, T)
     ctx.set_params(O.scene_params(), cas)
