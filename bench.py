@@ -69,13 +69,23 @@ def algorithmic_bytes(ctx):
     return {"pass_a": a, "pass_b": b, "frame": a + b, "cache_resident": resident}
 
 
-def pmc_traffic(kernel_substr, profiles_dir=os.path.join(ROOT, "profiles")):
-    """HBM bytes per launch of a kernel from the newest committed rocprofv3 PMC summary
-    (tools/profile.sh -> profiles/<round>/pmc_summary.json): 2 x FETCH_SIZE (gfx950 reports half
-    of wide streaming reads) + WRITE_SIZE.  None if no summary covers the kernel."""
+ROUND = "r03"  # profiles/<ROUND>*/ hold this round's profiler records and micro-benchmarks
+
+
+def _norm(sym):
+    return " ".join(sym.split()) if sym else sym
+
+
+def pmc_traffic(symbol, config, profiles_dir=os.path.join(ROOT, "profiles")):
+    """HBM bytes per launch of the kernel `symbol` (the exact demangled name of the kernel that ran,
+    ocean_kernel_name) from the newest committed rocprofv3 PMC summary of `config`
+    (tools/profile.sh -> profiles/<tag>/pmc_summary.json): 2 x FETCH_SIZE (gfx950 reports half of
+    wide streaming reads) + WRITE_SIZE.  (bytes, source dir) or None if no summary holds that
+    symbol."""
     best = None
-    if not os.path.isdir(profiles_dir):
+    if not symbol or not os.path.isdir(profiles_dir):
         return None
+    want = _norm(symbol)
     for d in sorted(os.listdir(profiles_dir)):
         f = os.path.join(profiles_dir, d, "pmc_summary.json")
         if not os.path.exists(f):
@@ -84,38 +94,47 @@ def pmc_traffic(kernel_substr, profiles_dir=os.path.join(ROOT, "profiles")):
             summ = json.load(open(f))
         except Exception:
             continue
+        if summ.get("config") != config:
+            continue
         for k, rec in summ.get("kernels", {}).items():
-            if kernel_substr in k and summ.get("config") == "cfg3":
+            if _norm(k) == want:
                 best = (rec["hbm_bytes_per_launch"], d)
     return best
 
 
-def rocprof_kernel_us(csv_name, kernel_substr, profiles_dir=os.path.join(ROOT, "profiles")):
-    """(average ns -> us, source) of a kernel from the newest committed rocprofv3 --stats
-    summary named `csv_name` under profiles/<round>/ (tools/r02_base.sh); None if absent."""
+def rocprof_kernel_us(csv_name, symbol, profiles_dir=os.path.join(ROOT, "profiles")):
+    """(average ns -> us, source) of the kernel `symbol` (exact demangled name) from the newest
+    committed rocprofv3 --stats summary named `csv_name` under profiles/<tag>/; None if absent."""
     import csv
     best = None
-    if not os.path.isdir(profiles_dir):
+    if not symbol or not os.path.isdir(profiles_dir):
         return None
+    want = _norm(symbol)
     for d in sorted(os.listdir(profiles_dir)):
         f = os.path.join(profiles_dir, d, csv_name)
         if not os.path.exists(f):
             continue
         for row in csv.DictReader(open(f)):
-            if kernel_substr in row["Name"]:
+            if _norm(row["Name"]) == want:
                 best = (float(row["AverageNs"]) / 1e3, f"profiles/{d}/{csv_name}")
     return best
 
 
+def _round_dirs(profiles_dir):
+    """This round's profile directories (profiles/<ROUND>*), oldest first: micro-benchmark
+    ceilings are quoted only when they were measured beside this round's kernels."""
+    if not os.path.isdir(profiles_dir):
+        return []
+    return [d for d in sorted(os.listdir(profiles_dir)) if d.startswith(ROUND)]
+
+
 def write_ceilings(profiles_dir=os.path.join(ROOT, "profiles")):
-    """Measured store-bandwidth ceilings of this chip from the newest committed tools/wrbench.hip run
-    (profiles/<round>/wrbench.txt): GB/s of nontemporal float4 stores over 192 MiB (pass B's texture
-    bytes) and beyond the Infinity Cache (1 GiB).  None if absent."""
+    """Measured store-bandwidth ceilings of this chip from this round's newest tools/wrbench.hip run
+    (profiles/<ROUND>*/wrbench.txt): GB/s of nontemporal float4 stores over 192 MiB (pass B's texture
+    bytes) and beyond the Infinity Cache (1 GiB).  None if this round has none."""
     import re
     best = None
-    if not os.path.isdir(profiles_dir):
-        return None
-    for d in sorted(os.listdir(profiles_dir)):
+    for d in _round_dirs(profiles_dir):
         f = os.path.join(profiles_dir, d, "wrbench.txt")
         if not os.path.exists(f):
             continue
@@ -131,14 +150,12 @@ def write_ceilings(profiles_dir=os.path.join(ROOT, "profiles")):
 
 
 def shape_us(fname, label, profiles_dir=os.path.join(ROOT, "profiles")):
-    """Microsecond time of the line starting with `label` in the newest committed
-    profiles/<round>/<fname> (tools/aqbench.hip, tools/bqbench.hip: a pass's memory shape run
+    """Microsecond time of the line starting with `label` in this round's newest
+    profiles/<ROUND>*/<fname> (tools/aqbench.hip, tools/bqbench.hip: a pass's memory shape run
     without its evolve / FFT work, 4 x 1024^2).  (us, source) or None."""
     import re
     best = None
-    if not os.path.isdir(profiles_dir):
-        return None
-    for d in sorted(os.listdir(profiles_dir)):
+    for d in _round_dirs(profiles_dir):
         f = os.path.join(profiles_dir, d, fname)
         if not os.path.exists(f):
             continue
@@ -173,6 +190,74 @@ def beyond_cache(steps=20):
                 "bytes_per_step": a + b, "ms_per_step": round(dt * 1e3, 4),
                 "achieved_GBs": round((a + b) / dt / 1e9, 1),
                 "frac": round((a + b) / dt / 1e9 / HBM_PEAK_GBS, 4)}
+    finally:
+        ctx.close()
+
+
+def ifft_measure(ctx, reps, csv_name, pmc_config):
+    """The operator IFFT (ocean_ifft2d over the 4 planes, IFFT.InverseFastFourierTransform x 4) of a
+    context: wall time (no events) and kernel time (HIP events attached to every launch) per call,
+    algorithmic bytes 32 B per texel per plane (two passes x read + write), the symbols of the row
+    and column kernels that ran, and the committed rocprofv3 / PMC records of exactly those symbols."""
+    n, units = ctx.n, ctx.C * ctx.T
+    for _ in range(3):  # first launches load the row/column code objects: keep them out of the timing
+        ctx.ifft2d(0b1111)
+    ctx.synchronize()
+    s0 = time.perf_counter()  # wall region: no events
+    for _ in range(reps):
+        ctx.ifft2d(0b1111)
+    ctx.synchronize()
+    s1 = time.perf_counter()
+    ctx.set_kernel_timing(True)  # kernel region: events around every launch
+    ctx.kernel_stats(0), ctx.kernel_stats(1), ctx.kernel_stats(2)
+    for _ in range(reps):
+        ctx.ifft2d(0b1111)
+    r_ms, r_n = ctx.kernel_stats(0)
+    c_ms, c_n = ctx.kernel_stats(1)
+    ctx.set_kernel_timing(False)
+    syms = {"rows": ctx.kernel_name(0), "cols": ctx.kernel_name(1)}
+    fft_bytes = 32 * n * n * 4 * units
+    stage_us = 1e6 * (s1 - s0) / reps
+    kern_us = 1e3 * (r_ms + c_ms) / reps
+    rp = {k: rocprof_kernel_us(csv_name, v) for k, v in syms.items()}
+    rocprof = None
+    if rp["rows"] and rp["cols"]:
+        # launches per call: rows and columns may run per unit chunk (ocean_abi.cpp)
+        lr, lc = r_n / reps, c_n / reps
+        rus = rp["rows"][0] * lr + rp["cols"][0] * lc
+        rocprof = {"source": rp["cols"][1], "rows_us": round(rp["rows"][0], 2), "cols_us": round(rp["cols"][0], 2),
+                   "launches_per_call": [lr, lc], "achieved_GBs": round(fft_bytes / (rus * 1e-6) / 1e9, 1),
+                   "frac": round(fft_bytes / (rus * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+    traffic = None
+    if pmc_config:
+        tr = {k: pmc_traffic(v, pmc_config) for k, v in syms.items()}
+        if tr["rows"] and tr["cols"]:
+            traffic = {"rows_bytes_per_launch": tr["rows"][0], "cols_bytes_per_launch": tr["cols"][0],
+                       "source": f"profiles/{tr['cols'][1]}/pmc_summary.json"}
+    return {"bytes": fft_bytes, "us_per_stage_wall": round(stage_us, 2), "us_per_stage_kernels": round(kern_us, 2),
+            "row_launches": r_n // reps, "col_launches": c_n // reps,
+            "rows_us": round(1e3 * r_ms / reps, 2), "cols_us": round(1e3 * c_ms / reps, 2),
+            "rows_frac": round(fft_bytes / 2 / (1e3 * r_ms / reps * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+            "cols_frac": round(fft_bytes / 2 / (1e3 * c_ms / reps * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+            "achieved_GBs": round(fft_bytes / (kern_us * 1e-6) / 1e9, 1),
+            "frac": round(fft_bytes / (kern_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+            "wall_frac": round(fft_bytes / (stage_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+            "symbols": syms, "rocprof": rocprof, "traffic": traffic}
+
+
+def ifft_beyond_cache(reps=20):
+    """The operator IFFT at N = 1024 on a plane set twice the 256 MiB Infinity Cache: 4 tiles x 4
+    cascades x 4 planes = 512 MiB, so the operator's bytes cannot all be
+    cache-resident between its launches."""
+    ctx = oh.OceanContext(1024, 4, 4, oh.F_UNFUSED)
+    try:
+        ctx.set_params(SCENE_PARAMS, SCENE_CASCADES)
+        ctx.generate_noise_device(20251121)
+        ctx.init_spectrum()
+        ctx.evolve(0.5)  # planes with the frame's data (the transform's time does not depend on it)
+        r = ifft_measure(ctx, reps, "ifft_bc_kernel_stats.csv", "ifft_bc")
+        r["workload"] = "4 tiles x 4 cascades x 1024^2, 4 planes: 512 MiB of planes (2x the Infinity Cache)"
+        return r
     finally:
         ctx.close()
 
@@ -234,6 +319,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ifft-stage", action="store_true")
     ap.add_argument("--no-beyond-cache", action="store_true")
+    ap.add_argument("--no-interleave", action="store_true",
+                    help="cfg5 past one GPU per cascade: contiguous column bands instead of even / odd columns")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -263,13 +350,15 @@ def main():
         tiles = cfg["tiles"]
         first = rank * tiles
         casc0, C, x0, nx = 0, cfg["cascades"], 0, n
+        parity = -1
         job_oceans = tiles * world
     else:
         # strong scaling: the job's fixed oceans split over the ranks -- contiguous tile
         # blocks (cfg4), or one ocean's cascades and then column bands (cfg5 on 8 GPUs:
         # one cascade, half the columns per rank); no data exchange either way
-        sh = plan_shard(cfg["tiles"], cfg["cascades"], n, world, rank)
+        sh = plan_shard(cfg["tiles"], cfg["cascades"], n, world, rank, interleave=not args.no_interleave)
         first, tiles, casc0, C, x0, nx = sh.tile0, sh.tiles, sh.casc0, sh.cascades, sh.x0, sh.nx
+        parity = sh.parity
         job_oceans = cfg["tiles"]
     flags = (oh.F_DISPLACEMENT_ONLY if cfg["disp_only"] else 0) | (oh.F_UNFUSED if args.unfused else 0)
 
@@ -280,7 +369,9 @@ def main():
     ctx = oh.OceanContext(n, C, tiles, flags, device=device)
     ctx.set_params(SCENE_PARAMS, SCENE_CASCADES[casc0:casc0 + C])
     ctx.generate_noise(tile_seed(20251121, first))  # the reference shares one noise texture over cascades
-    if nx != n:
+    if parity >= 0:
+        ctx.set_column_parity(parity)  # even / odd columns of the cascade (cfg5 on 8 GPUs)
+    elif nx != n:
         ctx.set_column_band(x0, nx)
     ctx.init_spectrum()
     ctx.synchronize()
@@ -357,47 +448,18 @@ def main():
         dom_bytes = n * n * units * 16 * (2 if cfg["disp_only"] else 4)
     achieved = dom_bytes / (dom_us * 1e-6) / 1e9 if dom_us > 0 else 0.0
 
+    kernel_syms = {"pass_a": ctx.kernel_name(0), "pass_b": ctx.kernel_name(1)}
+    dom_sym = kernel_syms["pass_b" if dom in ("pass_b", "ifft_cols") else "pass_a"]
+
     ifft_stage = None
     if not args.no_ifft_stage and not cfg["disp_only"]:
         # operator-level stage (IFFT.InverseFastFourierTransform x 4 planes), unfused kernels
-        for _ in range(3):  # first launches load the row/column code objects: keep them out of the timing
-            ctx.ifft2d(0b1111)
-        ctx.synchronize()
-        reps = max(20, args.steps // 5)
-        s0 = time.perf_counter()  # wall region: no events
-        for _ in range(reps):
-            ctx.ifft2d(0b1111)
-        ctx.synchronize()
-        s1 = time.perf_counter()
-        ctx.set_kernel_timing(True)  # kernel region: events around every launch
-        ctx.kernel_stats(0), ctx.kernel_stats(1), ctx.kernel_stats(2)
-        for _ in range(reps):
-            ctx.ifft2d(0b1111)
-        r_ms, r_n = ctx.kernel_stats(0)
-        c_ms, c_n = ctx.kernel_stats(1)
-        ctx.set_kernel_timing(False)
-        fft_bytes = 32 * n * n * 4 * units
-        stage_us = 1e6 * (s1 - s0) / reps
-        kern_us = 1e3 * (r_ms + c_ms) / reps
-        rp_r = rocprof_kernel_us("ifft_kernel_stats.csv", f"k_rows2<{n},")
-        rp_c = rocprof_kernel_us("ifft_kernel_stats.csv", f"k_cols2<{n}")
-        rocprof = None
-        if rp_r and rp_c and args.config == "cfg3":
-            rus = rp_r[0] + rp_c[0]
-            rocprof = {"source": rp_c[1], "rows_us": round(rp_r[0], 2), "cols_us": round(rp_c[0], 2),
-                       "achieved_GBs": round(fft_bytes / (rus * 1e-6) / 1e9, 1),
-                       "frac": round(fft_bytes / (rus * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
-        ifft_stage = {"bytes": fft_bytes, "us_per_stage_wall": round(stage_us, 2),
-                      "us_per_stage_kernels": round(kern_us, 2),
-                      "row_launch_us_4_planes": round(1e3 * r_ms / max(r_n, 1), 2),
-                      "col_launch_us_4_planes": round(1e3 * c_ms / max(c_n, 1), 2),
-                      "achieved_GBs": round(fft_bytes / (kern_us * 1e-6) / 1e9, 1),
-                      "frac": round(fft_bytes / (kern_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
-                      "rocprof": rocprof}
+        ifft_stage = ifft_measure(ctx, max(20, args.steps // 5), "ifft_kernel_stats.csv",
+                                  "cfg3" if args.config == "cfg3" else None)
+        if rank == 0 and world == 1 and args.config == "cfg3" and not args.no_beyond_cache:
+            ifft_stage["beyond_cache"] = ifft_beyond_cache()
 
-    traffic = pmc_traffic(("k_pass_b" if dom == "pass_b" else "k_pass_a") if not args.unfused
-                          else ("k_cols" if dom == "ifft_cols" else "k_rows")) \
-        if (args.config == "cfg3" and not args.unfused) else None
+    traffic = pmc_traffic(dom_sym, args.config) if not args.unfused else None
     # the dominant kernel's store stream against the chip's measured store ceiling: pass B writes the
     # textures (16 B DISP [+ 32 B DERIV, TURB] [+ 16 B NORMAL]) and the 4-B foam state per texel
     writes = None
@@ -444,7 +506,8 @@ def main():
             "data": "synthetic (scene parameters of Waves.unity, seeded noise 20251121+tile)",
             "config": {"workload": f"{args.config}: {cfg['desc']}", "n": n, "cascades": cfg["cascades"],
                        "tiles_per_gpu": tiles, "tiles_total": job_oceans,
-                       "rank0_shard": {"cascades": [casc0, casc0 + C], "columns": [x0, x0 + nx]},
+                       "rank0_shard": {"cascades": [casc0, casc0 + C],
+                                       "columns": f"x = 2m + {parity}" if parity >= 0 else [x0, x0 + nx]},
                        "schedule": "unfused" if args.unfused else "fused (pass A + pass B)",
                        "parallelism": f"{'independent oceans' if cfg['per_rank'] else 'one job split'} "
                                       f"over {world} GPU(s), no collective"},
@@ -452,6 +515,7 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic[0] if traffic else None,
                          "traffic_source": f"profiles/{traffic[1]}/pmc_summary.json" if traffic else None,
+                         "kernel_symbol": dom_sym,
                          "algorithmic_bytes_per_step": dom_bytes, "kernel_us_per_step": round(dom_us, 3),
                          "launches_per_step": round(launches_per_step, 2),
                          "writes": writes, "memory_shape": shape},

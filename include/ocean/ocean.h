@@ -48,7 +48,7 @@ extern "C" {
  *      return E_STATE before ocean_init_spectrum and the device entry checks alignment.
  *      New: ocean_reset_foam, ocean_set_column_band, ocean_sample_world(_device),
  *      ocean_read_async family, ocean_host_alloc/free, ocean_generate_noise_device,
- *      ocean_kernel_name. */
+ *      ocean_kernel_name, ocean_set_column_parity. */
 #define OCEAN_ABI_VERSION 2
 
 /* status codes */
@@ -171,6 +171,19 @@ int ocean_step(ocean_ctx *ctx, float time);
  * OCEAN_F_UNFUSED) and no OCEAN_F_MIPS; the unfused stages (ocean_evolve,
  * ocean_ifft2d, ocean_fill) ignore the band. */
 int ocean_set_column_band(ocean_ctx *ctx, int x_begin, int x_count);
+
+/* Column parity, the other way to split one unit over two GPUs (no reference
+ * counterpart): with parity b in {0, 1} the context computes only the output columns x = 2m + b,
+ * m < N/2, of every slice, by decimation in frequency of the row transform (each row is evolved
+ * whole, folded to z_b[n] = (a[n] + (-1)^b a[n + N/2]) e^{2 pi i b n / N} and transformed at N/2
+ * points), so the two ranks of a unit do not duplicate the row transform as column bands do.
+ * Column x = 2m + b is stored COMPACT at texture column m (DISP, DERIV, TURB, NORMAL: the first
+ * N/2 columns of each texture row; the rest are left as they are); the consumer interleaves the
+ * two ranks' textures.  Results equal the whole context's within the fp32 tolerance (a different
+ * radix order), not bit for bit.  N = 4096, fused full-output schedule, no OCEAN_F_MIPS; -1 turns
+ * it off (whole band again).  ocean_set_column_band replaces a parity; world sampling of a parity
+ * context returns OCEAN_E_UNSUPPORTED. */
+int ocean_set_column_parity(ocean_ctx *ctx, int parity);
 
 /* Replaces the TimeDependentSpectrum dispatch alone (WaterBody.cs:181-182;
  * TimeDependentSpectrum.compute:20-47): writes PLANE0..3 at `time`.  Async. */

@@ -97,6 +97,8 @@ namespace OceanHip
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
         public static extern OceanStatus ocean_set_column_band(IntPtr ctx, int xBegin, int xCount);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
+        public static extern OceanStatus ocean_set_column_parity(IntPtr ctx, int parity);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
         public static extern OceanStatus ocean_read_mip(IntPtr ctx, OceanTexture tex, int tile, int cascade, int level, [Out] float[] dst, UIntPtr bytes);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
         public static extern OceanStatus ocean_get_mip_ptr(IntPtr ctx, OceanTexture tex, int level, out IntPtr ptr, out UIntPtr sliceStride);

@@ -19,15 +19,19 @@ namespace ocean {
 namespace {
 
 // -------------------------------------------------------------- kernels
-constexpr int rows_per_item(int N) { return N >= 1024 ? 4 : 4096 / N; }
+// rows per workgroup of k_rows2: 4 at N = 1024 (1024 lanes); one row (256 lanes, 3 workgroups per CU)
+// at N = 2048 / 4096, where a 4-row image (128 / 256 KiB) held one workgroup per CU
+constexpr int rows_per_item(int N) { return N >= 2048 ? 1 : (N >= 1024 ? 4 : 4096 / N); }
 
 // Standalone row pass, in place: item = B consecutive rows of the flattened
 // [unit][y] row list of one plane.
+// `dst` may equal `plane` (in place) or be a scratch buffer of the same layout (the N >= 2048
+// four-step operator below).
 template <int N, int B = rows_per_item(N)>
-__global__ __launch_bounds__(B * N / kElems) void k_rows2(float2* __restrict__ plane, int total_rows,
+__global__ __launch_bounds__(B * N / kElems) void k_rows2(const float2* plane, float2* dst, int total_rows,
                                                          const float2* __restrict__ tw) {
-    using E = Engine<N, B, false, true>;
-    using TW = StageTw<N>;
+    using TW = StageTwLds<N>;
+    using E = Engine<N, B, false, true, 16, TW>;
     constexpr int T = E::THREADS;
     __shared__ float2 lds[E::LDS_ELEMS];
     __shared__ float2 twl[TW::kLdsEntries];
@@ -52,7 +56,7 @@ __global__ __launch_bounds__(B * N / kElems) void k_rows2(float2* __restrict__ p
     for (; item < items; item += gridDim.x) {
         const int next = item + gridDim.x;
         if (next < items) load(next, nxt);
-        const Win w = make_win(plane + (size_t)item * B * N, 0);
+        const Win w = make_win(dst + (size_t)item * B * N, 0);
         auto emit = [&](int m, int q, float2 val) {
             int b, j;
             E::template bj<E::RL>((int)threadIdx.x + m * T, b, j);
@@ -123,6 +127,159 @@ __global__ __launch_bounds__(W_ * N / kElems) void k_cols2(float2* __restrict__ 
     }
 }
 
+// ------------------------------------------------- four-step columns (N >= 2048)
+// The column transform of the operator at N = 2048 / 4096 as two passes over standard-layout
+// [y][x] unit-planes (the frame's fft4k.hip passes run on its tile-major intermediate instead):
+// N = L1 * L0, L1 = 64, y = y1 + L1 y0, k = k0 + L0 k1,
+//   C1 (in place): A[y1][k0] = w_N^(y1 k0) sum_y0 X[y1 + L1 y0] w_L0^(y0 k0), in the slot of X[y1 + L1 k0]
+//   C2 (out of place): Y[k0 + L0 k1] = sum_y1 A[y1][k0] w_L1^(y1 k1), then the permute.
+// A k_cols2 tile whose whole columns fit LDS at 4096 is 4 columns wide: 32-byte row pieces.  Here
+// every access is a 128-byte row piece (16 columns).  C2's outputs (rows k0 + L0 k1) are other
+// items' inputs (rows L1 k0 + y1), so the operator runs rows -> scratch, C1 on the scratch, C2
+// scratch -> plane, per chunk of unit-planes small enough to stay in the Infinity Cache.
+constexpr int kOpL1 = 64;                       // step-2 length
+constexpr int kOpW = 16;                        // columns per tile: 128-byte row pieces
+constexpr int kOpSeq = 64;                      // sequences per workgroup: 16 columns x 4 y1 (C1) / k0 (C2)
+constexpr int kOpBlk = kOpSeq / kOpW;           // y1 (C1) or k0 (C2) values per item
+
+// Per-stage tables of the L-point plan read from the context's N-point table tw[m] = exp(2 pi i m / N)
+// (the same float bits as the frame's fft4k.hip SubTw).
+template <int L, int N>
+struct OpSubTw {
+    using Full = StageTw<L, 16>;
+    static constexpr int S = Full::S;
+    static constexpr int kLdsEntries = Full::kEntries;
+    template <int s>
+    static __device__ __forceinline__ void load_stage(float2* lds, const float2* tw, int tid, int nthreads) {
+        if constexpr (s < S) {
+            constexpr int NS = ns_of(L, s, 16), R = radix_of(L, s, 16), O = Full::off(s);
+            for (int i = tid; i < NS * R; i += nthreads) {
+                const int r = i / NS, k = i % NS;
+                lds[O + i] = tw[(r * k * (N / (NS * R))) & (N - 1)];
+            }
+            load_stage<s + 1>(lds, tw, tid, nthreads);
+        }
+    }
+    static __device__ __forceinline__ void load(float2* lds, const float2* tw, int tid, int nthreads) {
+        load_stage<1>(lds, tw, tid, nthreads);
+    }
+    template <int ST>
+    static __device__ __forceinline__ void apply(float2* v, int j, const float2* tws) {
+        Full::template apply<ST>(v, j, tws);
+    }
+};
+
+// C1: item = (unit-plane, 16-column tile, block of 4 y1); sequence b = y1_local * 16 + column,
+// element y0 at row y1 + L1 y0.  `buf` holds `ups` unit-planes of N x N.
+template <int N>
+__global__ __launch_bounds__(kOpSeq * (N / kOpL1) / kElems) void k_opc1(float2* __restrict__ buf, int items,
+                                                                         const float2* __restrict__ tw) {
+    constexpr int L0 = N / kOpL1;
+    using CT = ColTile<L0, kOpSeq>;
+    using TW = OpSubTw<L0, N>;
+    using E = Engine<L0, kOpSeq, true, Engine<L0, kOpSeq, true, false>::seq_pad_ok(), 16, TW>;
+    constexpr int T = E::THREADS;
+    constexpr int TILES = N / kOpW;
+    constexpr int BLKS = kOpL1 / kOpBlk;  // y1 blocks per tile
+    constexpr int ES = kOpL1 * N;         // element (y0) stride in float2
+    __shared__ float2 lds[E::LDS_ELEMS];
+    __shared__ float2 twl[TW::kLdsEntries];
+    __shared__ float2 two[128];  // w_N^m = lo[m % 64] * hi[m / 64]
+    TW::load(twl, tw, threadIdx.x, T);
+    for (int i = threadIdx.x; i < 128; i += T) two[i] = tw[N + i];
+    const int lb = (int)threadIdx.x % kOpSeq, lj = (int)threadIdx.x / kOpSeq;
+    const int col = lb % kOpW, y1l = lb / kOpW;
+    const int voff = ((y1l + kOpL1 * lj) * N + col) * 8;  // lane's element from the item's base
+    auto item_base = [&](int item) {  // uniform: unit-plane, tile, first y1 of the item
+        const int blk = item % BLKS, ut = item / BLKS;
+        const int up = ut / TILES, t = ut % TILES;
+        return buf + (size_t)up * N * N + (size_t)blk * kOpBlk * N + t * kOpW;
+    };
+    auto base_of = [&](int item) { return item_base(item) + voff / 8; };
+    float2 cur[kElems], nxt[kElems];
+    auto load = [&](int item, float2 (&d)[kElems]) {
+        const int blk = item % BLKS, t = (item / BLKS) % TILES;
+        const Win w = make_win(item_base(item), (unsigned)((N * N - blk * kOpBlk * N - t * kOpW) * 8));
+#pragma unroll
+        for (int i = 0; i < kElems; ++i) d[i] = bload2(w, voff, CT::in_dy(i) * ES * 8);
+    };
+    int item = blockIdx.x;
+    if (item < items) load(item, cur);
+    __syncthreads();
+    for (; item < items; item += gridDim.x) {
+        const int next = item + gridDim.x;
+        if (next < items) load(next, nxt);
+        float2* dst = base_of(item);
+        const int y1 = (item % BLKS) * kOpBlk + y1l;
+        auto emit = [&](int m, int q, float2 val) {
+            const int dy = CT::out_dy(m, q);  // k0 - lj
+            const int mm = y1 * (lj + dy);    // < L1 * L0 = N
+            const float2 w = cmul(two[mm & 63], two[64 + (mm >> 6)]);
+            dst[(size_t)dy * ES] = cmul(val, w);
+        };
+        E::run_regs(cur, lds, twl, emit);
+#pragma unroll
+        for (int i = 0; i < kElems; ++i) cur[i] = nxt[i];
+        __syncthreads();
+    }
+}
+
+// C2: item = (unit-plane, 16-column tile, block of 4 k0); sequence b = k0_local * 16 + column,
+// element y1 at row L1 k0 + y1 of `src`; output row k0 + L0 k1 of `dst`, permuted.
+template <int N>
+__global__ __launch_bounds__(kOpSeq * kOpL1 / kElems) void k_opc2(const float2* __restrict__ src,
+                                                                 float2* __restrict__ dst, int items,
+                                                                 const float2* __restrict__ tw) {
+    constexpr int L0 = N / kOpL1;
+    using CT = ColTile<kOpL1, kOpSeq>;
+    using TW = OpSubTw<kOpL1, N>;
+    using E = Engine<kOpL1, kOpSeq, true, Engine<kOpL1, kOpSeq, true, false>::seq_pad_ok(), 16, TW>;
+    constexpr int T = E::THREADS;
+    constexpr int TILES = N / kOpW;
+    constexpr int BLKS = L0 / kOpBlk;  // k0 blocks per tile
+    __shared__ float2 lds[E::LDS_ELEMS];
+    __shared__ float2 twl[TW::kLdsEntries];
+    TW::load(twl, tw, threadIdx.x, T);
+    const int lb = (int)threadIdx.x % kOpSeq, lj = (int)threadIdx.x / kOpSeq;
+    const int col = lb % kOpW, k0l = lb / kOpW;
+    auto decode = [&](int item, int& up, int& x, int& k0) {
+        const int blk = item % BLKS, ut = item / BLKS;
+        up = ut / TILES;
+        x = (ut % TILES) * kOpW + col;
+        k0 = blk * kOpBlk + k0l;
+    };
+    float2 cur[kElems], nxt[kElems];
+    const int voff = ((kOpL1 * k0l + lj) * N + col) * 8;  // lane's element from the item's base
+    auto load = [&](int item, float2 (&d)[kElems]) {
+        const int blk = item % BLKS, ut = item / BLKS;
+        const int up = ut / TILES, t = ut % TILES;
+        const size_t o = (size_t)kOpL1 * kOpBlk * blk * N + t * kOpW;  // uniform: first k0 row, tile
+        const Win w = make_win(src + (size_t)up * N * N + o, (unsigned)(((size_t)N * N - o) * 8));
+#pragma unroll
+        for (int i = 0; i < kElems; ++i) d[i] = bload2(w, voff, CT::in_dy(i) * N * 8);
+    };
+    int item = blockIdx.x;
+    if (item < items) load(item, cur);
+    __syncthreads();
+    for (; item < items; item += gridDim.x) {
+        const int next = item + gridDim.x;
+        if (next < items) load(next, nxt);
+        int up, x, k0;
+        decode(item, up, x, k0);
+        const int y0 = k0 + L0 * lj;  // lane's first output row; element (m, q) adds L0 * out_dy
+        float2* out = dst + (size_t)up * N * N + (size_t)y0 * N + x;
+        auto emit = [&](int m, int q, float2 val) {
+            const int dy = CT::out_dy(m, q);
+            const float s = perm_sign(x, y0 + L0 * dy);
+            out[(size_t)L0 * dy * N] = make_float2(val.x * s, val.y * s);
+        };
+        E::run_regs(cur, lds, twl, emit);
+#pragma unroll
+        for (int i = 0; i < kElems; ++i) cur[i] = nxt[i];
+        __syncthreads();
+    }
+}
+
 // --------------------------------------------------------------- launch
 template <class K>
 int persistent_grid(K kernel, int threads, int items) {
@@ -146,42 +303,74 @@ hipError_t dispatch_n(int n, A... a) {
     return hipErrorInvalidValue;
 }
 
+// In-place row / column launches over `ups` consecutive unit-planes at `base` (plane p of unit u is
+// unit-plane p * U + u of the one plane allocation).
 template <int N>
 struct Rows2 {
     template <int B>
-    static hipError_t go_b(const DevView* v, int p, int np, hipStream_t s) {
+    static hipError_t go_b(const DevView* v, float2* base, int ups, hipStream_t s) {
         constexpr int T = B * N / kElems;
-        const int total = np * v->units * N;
+        const int total = ups * N;
         const int items = (total + B - 1) / B;
         const int g = persistent_grid(k_rows2<N, B>, T, items);
-        launch((k_rows2<N, B>), dim3(g), dim3(T), 0, s, v->plane[p], total, v->tw);
+        launch((k_rows2<N, B>), dim3(g), dim3(T), 0, s, (const float2*)base, base, total, v->tw);
         return hipGetLastError();
     }
-    static hipError_t go(const DevView* v, int p, int np, hipStream_t s) {
-        return go_b<rows_per_item(N)>(v, p, np, s);
+    static hipError_t go(const DevView* v, float2* base, int ups, hipStream_t s) {
+        return go_b<rows_per_item(N)>(v, base, ups, s);
     }
 };
 template <int N>
 struct Cols2 {
     template <int W, bool XP>
-    static hipError_t go_w(const DevView* v, int p, int np, hipStream_t s) {
+    static hipError_t go_w(const DevView* v, float2* base, int ups, hipStream_t s) {
         constexpr int T = W * N / kElems;
-        const int items = np * v->units * (N / W);
+        const int items = ups * (N / W);
         int g = persistent_grid(k_cols2<N, W, XP>, T, items);
         if (XP) g -= g % 16;  // halves of a tile on blocks b, b + 8 at every step of the item loop
-        launch((k_cols2<N, W, XP>), dim3(g), dim3(T), 0, s, v->plane[p], items, v->tw);
+        launch((k_cols2<N, W, XP>), dim3(g), dim3(T), 0, s, base, items, v->tw);
         return hipGetLastError();
     }
-    static hipError_t go(const DevView* v, int p, int np, hipStream_t s) {
+    static hipError_t go(const DevView* v, float2* base, int ups, hipStream_t s) {
         if constexpr (N == 1024) {
             // default: 8-column halves paired on one XCD (45.6 against 49.7 us for 4 x 1024^2 x 4 planes);
             // OCEAN_COLS2_XP=0 selects the 16-column tiles (A/B)
             static const int xp = std::getenv("OCEAN_COLS2_XP") ? std::atoi(std::getenv("OCEAN_COLS2_XP")) : 1;
-            if (xp) return go_w<8, true>(v, p, np, s);
+            if (xp) return go_w<8, true>(v, base, ups, s);
         }
-        return go_w<cols2_w(N), false>(v, p, np, s);
+        return go_w<cols2_w(N), false>(v, base, ups, s);
     }
 };
+// Four-step operator for N = 2048 / 4096 over `ups` consecutive unit-planes at `planes` (one
+// allocation: plane p of unit u is unit-plane p * U + u), through `scratch` (>= ups unit-planes).
+template <int N>
+struct Op4 {
+    static hipError_t go(const DevView* v, float2* planes, int ups, float2* scratch, int part, hipStream_t s) {
+        if constexpr (N < 2048) {
+            return hipErrorInvalidValue;
+        } else {
+            if (part == 0) {  // rows: planes -> scratch
+                constexpr int B = rows_per_item(N), T = B * N / kElems;
+                const int total = ups * N;
+                const int items = (total + B - 1) / B;
+                const int g = persistent_grid(k_rows2<N, B>, T, items);
+                launch((k_rows2<N, B>), dim3(g), dim3(T), 0, s, (const float2*)planes, scratch, total, v->tw);
+            } else if (part == 1) {  // C1 in place on the scratch
+                constexpr int T = kOpSeq * (N / kOpL1) / kElems;
+                const int items = ups * (N / kOpW) * (kOpL1 / kOpBlk);
+                const int g = persistent_grid(k_opc1<N>, T, items);
+                launch((k_opc1<N>), dim3(g), dim3(T), 0, s, scratch, items, v->tw);
+            } else {  // C2: scratch -> planes
+                constexpr int T = kOpSeq * kOpL1 / kElems;
+                const int items = ups * (N / kOpW) * ((N / kOpL1) / kOpBlk);
+                const int g = persistent_grid(k_opc2<N>, T, items);
+                launch((k_opc2<N>), dim3(g), dim3(T), 0, s, (const float2*)scratch, planes, items, v->tw);
+            }
+            return hipGetLastError();
+        }
+    }
+};
+
 template <int N>
 struct StageTwCount {
     static hipError_t go(size_t* out) {
@@ -199,11 +388,15 @@ size_t stage_twiddle_entries(int n) {
     return e;
 }
 
-hipError_t launch_ifft_rows_v2(const DevView& v, int p, int np, hipStream_t s) {
-    return dispatch_n<Rows2>(v.n, &v, p, np, s);
+hipError_t launch_ifft_rows_v2(const DevView& v, float2* base, int ups, hipStream_t s) {
+    return dispatch_n<Rows2>(v.n, &v, base, ups, s);
 }
-hipError_t launch_ifft_cols_v2(const DevView& v, int p, int np, hipStream_t s) {
-    return dispatch_n<Cols2>(v.n, &v, p, np, s);
+hipError_t launch_ifft_cols_v2(const DevView& v, float2* base, int ups, hipStream_t s) {
+    return dispatch_n<Cols2>(v.n, &v, base, ups, s);
+}
+hipError_t launch_ifft_four_step(const DevView& v, float2* planes, int ups, float2* scratch, int part, hipStream_t s) {
+    if (v.n != 2048 && v.n != 4096) return hipErrorInvalidValue;
+    return v.n == 2048 ? Op4<2048>::go(&v, planes, ups, scratch, part, s) : Op4<4096>::go(&v, planes, ups, scratch, part, s);
 }
 
 }  // namespace ocean

@@ -207,7 +207,7 @@ __global__ __launch_bounds__(kSeq * kL1 / kElems) void k_col4s2(DevView v, int i
             auto emit = [&](int m, int q, float2 val) {
                 const int i = m * RL + q;
                 const int dy = CT::out_dy(m, q);
-                const float s = perm_sign(x, y0 + L0 * dy);
+                const float s = perm_sign(x * v.xstr + v.xpar, y0 + L0 * dy);  // x: compact column under a parity
                 const float re = val.x * s, im = val.y * s;
                 const size_t to = (size_t)L0 * dy * N;  // compile-time row offset
                 if constexpr (Q) {

@@ -180,6 +180,31 @@ struct StageTwCompact {
     }
 };
 
+// The compact tables of an L-point plan (R0 first) inside a context of size N > L, built from the
+// context's base table tw[m] = exp(2 pi i m / N) (the per-stage global tables are the N-point
+// plan's): entry (s, r, k) = tw[r k N / (Ns R)].  Pass A3P (fftq.hip) runs 2048-point transforms
+// in a 4096 context.
+template <int L, int N, int R0>
+struct StageTwCompactSub : StageTwCompact<L, R0> {
+    using Base = StageTwCompact<L, R0>;
+    template <int s>
+    static __device__ __forceinline__ void load_stage(float2* lds, const float2* tw, int tid, int nthreads) {
+        if constexpr (s < Base::S) {
+            constexpr int NS = ns_of(L, s, R0), R = radix_of(L, s, R0), RW = Base::rows(s), O = Base::off(s);
+            constexpr bool CP = Base::compact(s);
+            for (int i = tid; i < NS * RW; i += nthreads) {
+                const int row = i / NS, k = i % NS;
+                const int r = CP ? (1 << row) : row;
+                lds[O + i] = tw[(r * k * (N / (NS * R))) & (N - 1)];
+            }
+            load_stage<s + 1>(lds, tw, tid, nthreads);
+        }
+    }
+    static __device__ __forceinline__ void load(float2* lds, const float2* __restrict__ tw, int tid, int nthreads) {
+        load_stage<1>(lds, tw, tid, nthreads);
+    }
+};
+
 // LDS twiddle tables for plan (N, R0): the full per-stage tables when they fit, else the compact form.
 template <int N, int R0 = 16>
 using StageTwLds = std::conditional_t<StageTw<N, R0>::kInLds, StageTw<N, R0>, StageTwCompact<N, R0>>;

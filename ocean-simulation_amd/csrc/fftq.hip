@@ -32,6 +32,17 @@
 #ifndef AQ_SKIP
 #define AQ_SKIP 1  // pass AQ's idle pass-1 waves skip the stages (A/B builds)
 #endif
+#ifndef A3P_EARLY_PF
+#define A3P_EARLY_PF 1
+#endif
+#ifndef OCEAN_A3P_WPEU
+#define OCEAN_A3P_WPEU 0  // waves per SIMD pass A3P is compiled for (0: the compiler's choice; A/B builds)
+#endif
+#if OCEAN_A3P_WPEU
+#define A3P_WPEU __attribute__((amdgpu_waves_per_eu(OCEAN_A3P_WPEU)))
+#else
+#define A3P_WPEU
+#endif
 #if OCEAN_AQ_WPEU
 #define AQ_WPEU __attribute__((amdgpu_waves_per_eu(OCEAN_AQ_WPEU)))
 #else
@@ -347,6 +358,121 @@ __global__ __launch_bounds__(N / 4) void k_pass_a3q(DevView v, float time, int t
     }
 }
 
+// Pass A3P (N = 4096, column parity b = v.xpar, ocean_set_column_parity): the row pass of a rank
+// that owns the columns x = 2m + b.  With X[x] = sum_n a[n] e^{2 pi i n x / N} and n = n' + (N/2) h,
+//   X[2m + b] = sum_{n' < N/2} z_b[n'] e^{2 pi i n' m / (N/2)},  z_b[n'] = (a[n'] + (-1)^b a[n' + N/2]) w_N^{b n'}
+// (decimation in frequency), so the rank evolves the whole row (its h0 is read whole either way),
+// forms z_b of each of the four sequences with one radix-2 butterfly in registers and runs an
+// N/2-point transform instead of the N-point one: half the butterflies and LDS traffic of pass A3Q.
+// Lane j (N/8 lanes) evolves texels j + r N/8, r < 8; texels r and r + 4 give z_b[j + r N/8], r < 4:
+// stage-0 butterfly j of the N/2-point plan with first radix 4 (the engine of pass A3Q at N/2).
+// Outputs m < N/2 go to intermediate column m (compact); srow likewise.  d0 is per row (texel 0).
+template <int N, bool EARLY_PF = A3P_EARLY_PF>
+__global__ __launch_bounds__(N / 8) A3P_WPEU void k_pass_a3p(DevView v, float time, int total_rows) {
+    constexpr int H = N / 2;  // transform length
+    constexpr int FIRST = 4;
+    using TW = StageTwCompactSub<H, N, FIRST>;
+    using E = Engine<H, 4, false, true, FIRST, TW>;
+    constexpr int T = E::THREADS;
+    constexpr int R0 = E::R0;
+    constexpr int NJ = H / R0;  // lanes = texel stride
+    constexpr int W = inter_w(N);
+    constexpr int TILES = N / W;
+    constexpr int NSL = H / E::RL;
+    static_assert(T == NJ && R0 == 4 && T == N / 8, "lane j <-> stage-0 butterfly j of each sequence");
+    __shared__ float2 lds[E::LDS_ELEMS];
+    __shared__ float2 twl[TW::kLdsEntries];
+    TW::load(twl, v.tw, threadIdx.x, T);
+    const float2* tws = twl;
+    __shared__ WaveBand band[kMaxCascades];
+    if ((int)threadIdx.x < v.C) band[threadIdx.x] = wave_band(v.casc + threadIdx.x * 5);
+    const int j = (int)threadIdx.x;
+    const bool j0 = (j == 0);
+    const int par = v.xpar;
+    const float sgn = par ? -1.0f : 1.0f;
+    float4 h[2 * R0];
+    auto load = [&](int item, float4* hh) {
+        const Win w = make_win(v.h0 + (size_t)item * N, (unsigned)(N * 16));
+#pragma unroll
+        for (int r = 0; r < 2 * R0; ++r) hh[r] = bload4(w, j * 16, r * NJ * 16);
+    };
+    // twiddles w_N^{b n'} of the lane's z elements n' = j + r NJ (b = 1; 1 for b = 0)
+    float2 zt[R0];
+#pragma unroll
+    for (int r = 0; r < R0; ++r) zt[r] = par ? v.tw[j + r * NJ] : make_float2(1.0f, 0.0f);
+    int item = (gridDim.x % 8 == 0) ? (int)(blockIdx.x % 8) * (int)(gridDim.x / 8) + (int)blockIdx.x / 8
+                                    : (int)blockIdx.x;
+    if (item < total_rows) load(item, h);
+    __syncthreads();  // twiddles, band
+    for (; item < total_rows; item += gridDim.x) {
+        const int u = item / N, y = item % N;
+        const WaveBand wb = band[(u + v.c0) % v.C];
+        float2 in[4 * R0];  // slot p * R0 + r: sequence p, stage-0 input r (z_b[j + r NJ])
+#pragma unroll
+        for (int r = 0; r < R0; ++r) {
+            float2 qv[2][4];  // texel j + r NJ (lo) and j + (r + 4) NJ (hi): Q1..Q3 and row 0's Q4
+#pragma unroll
+            for (int hi = 0; hi < 2; ++hi) {
+                const int rr = r + hi * R0;
+                const float4 wd = wave_data(j + rr * NJ, y, N, wb, v.gravity);
+                const float2 hh = evolve_h(h[rr], evolve_phase(wd.w, time));
+                QTex qa, qb;
+                qv[hi][3] = make_float2(0.0f, 0.0f);
+                if (y != 0 && !(rr == 0 && j0)) {
+                    q_fast(hh, wd, qa, qb);
+                } else {  // Nyquist lines (see pass AQ)
+                    const float4 wm = make_float4((j0 && rr == 0) ? wd.x : -wd.x, wd.y, y ? -wd.z : wd.z, wd.w);
+                    const Planes4 o = planes_of(hh, wd), om = planes_of(make_float2(hh.x, -hh.y), wm);
+                    q_planes(o, om, qa, qb);
+                    if (y == 0) qv[hi][3] = q4_full(o, om);
+                    if (rr == 0 && j0) q_side(v, u)[y] = q4_minus(o, om, wd.z);
+                }
+#pragma unroll
+                for (int p = 0; p < 3; ++p) qv[hi][p] = qa.q[p];
+            }
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                const float2 zs = make_float2(qv[0][p].x + sgn * qv[1][p].x, qv[0][p].y + sgn * qv[1][p].y);
+                in[p * R0 + r] = par ? cmul(zs, zt[r]) : zs;
+            }
+        }
+        const int next = item + gridDim.x;
+        if (EARLY_PF && next < total_rows) load(next, h);  // the next row's h0 in flight across this row's stages
+        auto put = [&](int b, int jj, int q, float2 val) {
+            const int m = jj + q * NSL;  // compact column: x = 2 m + b
+            if (b == 3) {
+                if (y == 0) q_side(v, u)[N + m] = val;  // srow
+                return;
+            }
+            float2* rowp = v.tplane + (size_t)b * v.inter_stride + ((size_t)u * TILES * N + y) * W;
+            float2* dst = rowp + (size_t)(jj / W) * N * W + (jj % W);
+            dst[(size_t)q * (NSL / W) * N * W] = val;
+        };
+#pragma unroll
+        for (int p = 0; p < 4; ++p) Idft<R0>::run(&in[p * R0]);
+        // pass 0: Q1..Q3 (sequence slot 3 idle); row 0 only, pass 1: srow's input in slot 0
+        for (int ps = 0; ps < (y == 0 ? 2 : 1); ++ps) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                if (ps && p) continue;
+                float2* dst = lds + E::lidx(p, j * R0);
+#pragma unroll
+                for (int q = 0; q < R0; ++q) dst[E::loff(q, 1)] = in[(ps ? 3 : p) * R0 + q];
+            }
+            __syncthreads();
+            auto emit = [&](int m, int q, float2 val) {
+                int b, jj;
+                E::template bj<E::RL>((int)threadIdx.x + m * T, b, jj);
+                put(ps ? 3 : b, jj, q, val);
+            };
+            E::template stages_from<1>(lds, tws, emit, ps ? 1 : 3);
+            if (y == 0) __syncthreads();  // LDS reused by pass 1
+        }
+        __syncthreads();
+        if (!EARLY_PF && next < total_rows) load(next, h);
+    }
+}
+
 // Pass BQ: per (unit, W-column tile), four column transforms from three planes:
 //   step 0: R[Q2] -> (Dy, Dyx)          kept (LDS)
 //   step 1: R[Q1] -> (Dx, Dz)           DISP = (Dx, Dy, Dz, 1); Dyx moves to registers; before the
@@ -562,6 +688,14 @@ bool pass_q_supported(int n, int planes) {
 
 hipError_t launch_pass_a_q(const DevView& v, float t, hipStream_t s) {
     if (!pass_q_supported(v.n, v.planes) || !v.qside) return hipErrorInvalidValue;
+    if (v.xstr == 2) {  // column parity (even / odd columns of every row)
+        if (v.n != 4096 || v.x0 != 0 || v.nx != v.n / 2) return hipErrorInvalidValue;
+        constexpr int T = 4096 / 8;
+        const int total = v.units * 4096;
+        const int g = grid_q(k_pass_a3p<4096>, T, total);
+        launch((k_pass_a3p<4096>), dim3(g), dim3(T), 0, s, v, t, total);
+        return hipGetLastError();
+    }
     switch (v.n) {
         case 512: return v.h0k ? go_aq<512>(v, t, s) : hipErrorInvalidValue;
         case 1024: return v.h0k ? go_aq<1024>(v, t, s) : hipErrorInvalidValue;

@@ -11,6 +11,7 @@
 #include <new>
 #include <algorithm>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <tuple>
 #include <string>
@@ -96,6 +97,39 @@ namespace ocean {
 void generate_noise_host(int n, uint64_t seed, float* out);
 }
 
+// Device staging slots of ocean_read_async, each as large as one slice of the largest texture.  A
+// request takes a slot and gives it back when it is released (after its host copy has landed), so a
+// slot is never rewritten while a copy out of it is pending, and no allocation or free sits between
+// the context stream and the copy stream.  Shared with the requests: it outlives a context destroyed
+// before its requests are released.
+struct StagePool {
+    int device = 0;
+    size_t slot_bytes = 0;
+    std::mutex mu;
+    std::vector<void*> free_slots, all;
+    ~StagePool() {
+        (void)hipSetDevice(device);
+        for (void* p : all) (void)hipFree(p);
+    }
+    hipError_t take(void** out) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (free_slots.empty()) {
+            void* p = nullptr;
+            const hipError_t e = hipMalloc(&p, slot_bytes);
+            if (e != hipSuccess) return e;
+            all.push_back(p);
+            free_slots.push_back(p);
+        }
+        *out = free_slots.back();
+        free_slots.pop_back();
+        return hipSuccess;
+    }
+    void give(void* p) {
+        std::lock_guard<std::mutex> lk(mu);
+        free_slots.push_back(p);
+    }
+};
+
 struct ocean_ctx {
     int device = 0;
     int n = 0, logn = 0, C = 0, T = 0, P = 4;
@@ -113,8 +147,11 @@ struct ocean_ctx {
     int c4_bands = 0;        // OCEAN_C4_BANDS: N >= 2048 column passes per (unit, band); 0 = auto
     int chunk_min = 1 << 30; // OCEAN_CHUNK_MIN: units per chunk when one unit exceeds OCEAN_CHUNK_MIB
     int chunk_reuse = 1;     // OCEAN_CHUNK_REUSE=0: one intermediate region per unit (A/B)
+    int op_four_step = 1;    // OCEAN_OP_FOUR_STEP=0: ocean_ifft2d at N >= 2048 through k_rows2 / k_cols2 (A/B)
+    long op_chunk_mib = 0;   // OCEAN_OP_CHUNK_MIB: MiB of unit-planes per chunk of the operator IFFT (0: auto)
     size_t inter_units = 0;  // units the intermediate holds (a chunk's, or all with chunk_reuse = 0)
     int band_x0 = 0, band_nx = 0;  // column band of the fused passes (ocean_set_column_band); nx = n: whole
+    int col_par = -1;              // column parity (ocean_set_column_parity): -1 off, else x = 2 m + col_par
     int tile_w = 8;                // column-tile width of the fused path's tile-major layouts (ocean_create)
     float4* waves = nullptr;
     float2* plane[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -131,6 +168,7 @@ struct ocean_ctx {
     float4* turb_mips = nullptr;
     size_t mip_chain = 0;
     hipStream_t copy_stream = nullptr;  // ocean_read_async
+    std::shared_ptr<StagePool> stage_pool;  // ocean_read_async staging slots
     // host state.  `params` and the device `casc` are what the kernels run with; set_params
     // only stages new values, which ocean_init_spectrum makes active (ocean.h), so a
     // frame stepped between the two still uses the spectrum's own constants.
@@ -184,6 +222,8 @@ struct ocean_ctx {
         v.mip_chain = mip_chain;
         v.x0 = band_x0;
         v.nx = band_nx;
+        v.xstr = col_par >= 0 ? 2 : 1;
+        v.xpar = col_par >= 0 ? col_par : 0;
         return v;
     }
 
@@ -368,6 +408,8 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
     if (const char* kb = std::getenv("OCEAN_C4_BANDS")) c->c4_bands = std::max(0, std::atoi(kb));
     if (const char* km = std::getenv("OCEAN_CHUNK_MIN")) c->chunk_min = std::max(1, std::atoi(km));
     if (const char* kr = std::getenv("OCEAN_CHUNK_REUSE")) c->chunk_reuse = std::atoi(kr);
+    if (const char* kf = std::getenv("OCEAN_OP_FOUR_STEP")) c->op_four_step = std::atoi(kf);
+    if (const char* ko = std::getenv("OCEAN_OP_CHUNK_MIB")) c->op_chunk_mib = std::max(0L, std::atol(ko));
     // Width of the fused path's column tiles.  With fewer tiles than CUs (one 512^2
     // cascade: 32 tiles of 16 columns) pass B ran on an eighth of the chip, so small
     // jobs at N <= 512 take 4-column tiles (at N = 1024 pass A's
@@ -571,6 +613,7 @@ int ocean_ifft2d(ocean_ctx* ctx, int plane_mask) {
         if ((plane_mask & (1 << p)) && p >= ctx->P)
             return fail(OCEAN_E_INVALID_ARG, "plane not allocated (DISPLACEMENT_ONLY context)");
     const ocean::DevView v = ctx->view();
+    const size_t up_elems = ctx->texels();  // one unit-plane
     for (int p = 0; p < 4;) {
         if (!(plane_mask & (1 << p))) {
             ++p;
@@ -578,10 +621,47 @@ int ocean_ifft2d(ocean_ctx* ctx, int plane_mask) {
         }
         int np = 1;  // run of consecutive planes: one launch per direction (planes are one allocation)
         while (p + np < 4 && (plane_mask & (1 << (p + np)))) ++np;
-        if (int r = timed(ctx, 0, [&] { return ocean::launch_ifft_rows_v2(v, p, np, ctx->stream); }, "ifft_rows"))
-            return r;
-        if (int r = timed(ctx, 1, [&] { return ocean::launch_ifft_cols_v2(v, p, np, ctx->stream); }, "ifft_cols"))
-            return r;
+        if (ctx->n >= 2048 && ctx->op_four_step) {
+            // four-step columns (fft2.hip): per chunk of unit-planes, rows -> scratch (the fused
+            // intermediate's room), C1 on the scratch, C2 scratch -> planes; a chunk of at most
+            // OCEAN_OP_CHUNK_MIB stays in the Infinity Cache between the three launches
+            const int ups = np * (int)ctx->units();
+            const size_t scratch_ups = ctx->inter_units * ctx->P;
+            // auto: 128 MiB, one 4096^2 unit-plane (two: 2.80 against 2.19 ms for 4 x 4096^2 x 4 planes)
+            const long mib = ctx->op_chunk_mib > 0 ? ctx->op_chunk_mib : 128;
+            int k = (int)std::max<size_t>(1, ((size_t)mib << 20) / (up_elems * 8));
+            k = (int)std::min<size_t>((size_t)k, scratch_ups);
+            for (int c0 = 0; c0 < ups; c0 += k) {
+                const int kc = std::min(k, ups - c0);
+                float2* planes = ctx->plane[p] + (size_t)c0 * up_elems;
+                if (int r = timed(ctx, 0, [&] {
+                        return ocean::launch_ifft_four_step(v, planes, kc, ctx->tplane, 0, ctx->stream);
+                    }, "ifft_rows"))
+                    return r;
+                if (int r = timed(ctx, 1, [&] {
+                        hipError_t e = ocean::launch_ifft_four_step(v, planes, kc, ctx->tplane, 1, ctx->stream);
+                        return e != hipSuccess ? e : ocean::launch_ifft_four_step(v, planes, kc, ctx->tplane, 2, ctx->stream);
+                    }, "ifft_cols"))
+                    return r;
+            }
+            p += np;
+            continue;
+        }
+        // N <= 1024: in-place row and column launches per chunk of at most OCEAN_OP_CHUNK_MIB of
+        // unit-planes, so the column launch re-reads the rows' output from the Infinity Cache when the
+        // plane set is larger than it.  Auto: 256 MiB (4 x 4 x 1024^2 x 4 planes, 512 MiB: 64 / 128 /
+        // 192 / 256 MiB / unchunked 0.66 / 0.70 / 0.71 / 0.735 / 0.54 of peak; cfg3's 128 MiB: one chunk)
+        const int ups = np * (int)ctx->units();
+        const long mib = ctx->op_chunk_mib > 0 ? ctx->op_chunk_mib : 256;
+        const int k = (int)std::max<size_t>(1, ((size_t)mib << 20) / (up_elems * 8));
+        for (int c0 = 0; c0 < ups; c0 += k) {
+            const int kc = std::min(k, ups - c0);
+            float2* base = ctx->plane[p] + (size_t)c0 * up_elems;
+            if (int r = timed(ctx, 0, [&] { return ocean::launch_ifft_rows_v2(v, base, kc, ctx->stream); }, "ifft_rows"))
+                return r;
+            if (int r = timed(ctx, 1, [&] { return ocean::launch_ifft_cols_v2(v, base, kc, ctx->stream); }, "ifft_cols"))
+                return r;
+        }
         p += np;
     }
     return OCEAN_OK;
@@ -683,6 +763,8 @@ int step_fused(ocean_ctx* ctx, float time) {
     // rows; pass B: column tiles (N <= 1024) or the four-step column passes (N >= 2048)
     const ocean::DevView v = ctx->view();
     const bool q = use_q(ctx);
+    if (ctx->col_par >= 0 && !q)
+        return fail(OCEAN_E_STATE, "a column parity needs the three-plane frame (h0 from ocean_init_spectrum)");
     const int U = (int)ctx->units(), K = std::min(chunk_units(ctx, q ? q_planes(ctx) : ctx->P), (int)ctx->inter_units);
     for (int u0 = 0; u0 < U; u0 += K) {
         const ocean::DevView c = (K >= U) ? v : sub_view(v, u0, std::min(K, U - u0), ctx->inter_units < ctx->units());
@@ -796,8 +878,11 @@ int ocean_get_mip_ptr(ocean_ctx* ctx, int texture, int level, void** ptr, size_t
 }  // extern "C"
 
 struct ocean_readback {
-    hipEvent_t done = nullptr;
+    hipEvent_t done = nullptr;   // the host copy has landed
+    hipEvent_t after = nullptr;  // the snapshot is in the slot (the copy stream waits for it)
     int device = 0;
+    void* slot = nullptr;
+    std::shared_ptr<StagePool> pool;
 };
 
 extern "C" {
@@ -811,27 +896,32 @@ int ocean_read_async(ocean_ctx* ctx, int texture, int tile, int cascade, void* d
     char* src = nullptr;
     if (int r = slice_ptr(ctx, texture, tile, cascade, bytes, &src)) return r;
     if (!ctx->copy_stream) OCEAN_HIP(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+    if (!ctx->stage_pool) {
+        ctx->stage_pool = std::make_shared<StagePool>();
+        ctx->stage_pool->device = ctx->device;
+        ctx->stage_pool->slot_bytes = ctx->texels() * 16;  // the largest slice (float4 textures)
+    }
     ocean_readback* rb = new (std::nothrow) ocean_readback();
     if (!rb) return fail(OCEAN_E_OUT_OF_MEMORY, "host allocation failed");
     rb->device = ctx->device;
-    // Snapshot semantics, like a readback in Unity's command stream: a device-side
-    // copy into a staging buffer on the ctx stream (ordered after the queued steps
-    // and before later ones, ~16 MiB at HBM speed), then the host copy on the copy
-    // stream, off the ctx stream's critical path.
-    hipEvent_t after = nullptr;
-    void* stage = nullptr;
-    hipError_t e = hipEventCreateWithFlags(&after, hipEventDisableTiming);
+    rb->pool = ctx->stage_pool;
+    // Snapshot semantics, like a readback in Unity's command stream: a device-side copy into a
+    // staging slot on the ctx stream (ordered after the queued steps and before later ones,
+    // ~16 MiB at HBM speed), then the host copy on the copy stream, off the ctx stream's path.
+    hipError_t e = hipEventCreateWithFlags(&rb->after, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&rb->done, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipMallocAsync(&stage, bytes, ctx->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(stage, src, bytes, hipMemcpyDeviceToDevice, ctx->stream);
-    if (e == hipSuccess) e = hipEventRecord(after, ctx->stream);
-    if (e == hipSuccess) e = hipStreamWaitEvent(ctx->copy_stream, after, 0);
-    if (e == hipSuccess) e = hipMemcpyAsync(dst, stage, bytes, hipMemcpyDeviceToHost, ctx->copy_stream);
-    if (e == hipSuccess) e = hipFreeAsync(stage, ctx->copy_stream);
+    if (e == hipSuccess) e = rb->pool->take(&rb->slot);
+    if (e == hipSuccess) e = hipMemcpyAsync(rb->slot, src, bytes, hipMemcpyDeviceToDevice, ctx->stream);
+    if (e == hipSuccess) e = hipEventRecord(rb->after, ctx->stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(ctx->copy_stream, rb->after, 0);
+    if (e == hipSuccess) e = hipMemcpyAsync(dst, rb->slot, bytes, hipMemcpyDeviceToHost, ctx->copy_stream);
     if (e == hipSuccess) e = hipEventRecord(rb->done, ctx->copy_stream);
-    if (after) (void)hipEventDestroy(after);  // destruction is deferred until the wait has been resolved
     if (e != hipSuccess) {
+        (void)hipStreamSynchronize(ctx->copy_stream);
+        (void)hipStreamSynchronize(ctx->stream);
+        if (rb->slot) rb->pool->give(rb->slot);
         if (rb->done) (void)hipEventDestroy(rb->done);
+        if (rb->after) (void)hipEventDestroy(rb->after);
         delete rb;
         return hip_fail(e, "ocean_read_async");
     }
@@ -855,8 +945,11 @@ int ocean_readback_wait(ocean_readback* rb) {
 
 void ocean_readback_release(ocean_readback* rb) {
     if (!rb) return;
-    (void)hipEventSynchronize(rb->done);
+    (void)hipSetDevice(rb->device);
+    (void)hipEventSynchronize(rb->done);  // the slot is free only once its host copy has landed
     (void)hipEventDestroy(rb->done);
+    (void)hipEventDestroy(rb->after);
+    rb->pool->give(rb->slot);
     delete rb;
 }
 
@@ -931,6 +1024,7 @@ static int check_sample(ocean_ctx* ctx, int tile, const float* pts, int count, f
 
 int ocean_sample_world_device(ocean_ctx* ctx, int tile, const float* points, int count, float* out) {
     if (int r = check_sample(ctx, tile, points, count, out)) return r;
+    if (ctx->col_par >= 0) return fail(OCEAN_E_UNSUPPORTED, "world sampling of a column-parity shard (half the columns)");
     // k_sample_world reads floats and writes float4 rows (ocean.h)
     if (((uintptr_t)points & 3) || ((uintptr_t)out & 15))
         return fail(OCEAN_E_INVALID_ARG, "ocean_sample_world_device: points must be 4-byte and out 16-byte aligned");
@@ -973,6 +1067,26 @@ int ocean_set_column_band(ocean_ctx* ctx, int x_begin, int x_count) {
         return fail(OCEAN_E_UNSUPPORTED, "a column band needs the fused schedule and no mip chains");
     ctx->band_x0 = x_begin;
     ctx->band_nx = x_count;
+    ctx->col_par = -1;  // a band replaces a column parity
+    return OCEAN_OK;
+}
+
+int ocean_set_column_parity(ocean_ctx* ctx, int parity) {
+    if (int r = enter(ctx)) return r;
+    if (parity < -1 || parity > 1) return fail(OCEAN_E_INVALID_ARG, "parity must be -1 (off), 0 or 1");
+    if (parity < 0) {
+        ctx->col_par = -1;
+        ctx->band_x0 = 0;
+        ctx->band_nx = ctx->n;
+        return OCEAN_OK;
+    }
+    if (ctx->n != 4096) return fail(OCEAN_E_UNSUPPORTED, "a column parity is built for N = 4096 (pass A3P)");
+    if (ctx->flags & (OCEAN_F_UNFUSED | OCEAN_F_MIPS | OCEAN_F_DISPLACEMENT_ONLY))
+        return fail(OCEAN_E_UNSUPPORTED, "a column parity needs the fused full-output schedule and no mip chains");
+    if (!ctx->q) return fail(OCEAN_E_UNSUPPORTED, "a column parity needs the three-plane frame (OCEAN_Q=0 is set)");
+    ctx->col_par = parity;
+    ctx->band_x0 = 0;
+    ctx->band_nx = ctx->n / 2;  // compact: column m of every texture holds x = 2 m + parity
     return OCEAN_OK;
 }
 
@@ -1004,6 +1118,7 @@ int ocean_step_bytes(ocean_ctx* ctx, uint64_t* pass_a, uint64_t* pass_b) {
         // fill: P planes [+ foam state read + write] -> outputs
         a = tex * (32 + 8 * P + 16 * P);
         b = tex * (16 * P + 8 * P + (full ? 8 : 0) + outs);
+        if (ctx->n >= 2048 && ctx->op_four_step) b += tex * 16 * P;  // four-step columns: C1 and C2
     } else {
         const bool a4 = ctx->a4 && ctx->h0k_valid && ocean::pass_a4_supported(ctx->n, ctx->P);
         // column band: h0 is read whole (rows are transformed whole), the rest scales with the band

@@ -75,6 +75,9 @@ struct DevView {
     // multiples of the tile widths, full band = (0, N)
     int x0, nx;
     int c0;  // cascade of unit 0 of this view (a sub-view of a unit chunk may start mid-tile)
+    // column parity (ocean_set_column_parity): the context computes the columns x = xstr * m + xpar and
+    // stores column x at texture / intermediate column m < N / xstr; xstr = 1, xpar = 0 when off
+    int xstr, xpar;
 };
 
 struct SpectrumParams {
@@ -99,9 +102,14 @@ hipError_t launch_noise(const DevView& v, uint64_t seed, hipStream_t s);
 // software-pipelined row and column(+permute) launches, in place.
 // Entries of the per-stage twiddle tables stored at tw + N + 128 (see fft_engine.h StageTw).
 size_t stage_twiddle_entries(int n);
-// Each launch covers `np` consecutive planes p .. p+np-1 (one allocation).
-hipError_t launch_ifft_rows_v2(const DevView& v, int p, int np, hipStream_t s);
-hipError_t launch_ifft_cols_v2(const DevView& v, int p, int np, hipStream_t s);
+// Each launch covers `ups` consecutive unit-planes from `base` (plane p of unit u is unit-plane
+// p * U + u of the one plane allocation), in place.
+hipError_t launch_ifft_rows_v2(const DevView& v, float2* base, int ups, hipStream_t s);
+hipError_t launch_ifft_cols_v2(const DevView& v, float2* base, int ups, hipStream_t s);
+// N = 2048 / 4096: the operator over `ups` consecutive unit-planes at `planes` (plane p of unit u is
+// unit-plane p * U + u) through `scratch`; part 0 = rows (planes -> scratch), 1 = four-step column
+// step 1 (in place on scratch), 2 = step 2 + permute (scratch -> planes).
+hipError_t launch_ifft_four_step(const DevView& v, float2* planes, int ups, float2* scratch, int part, hipStream_t s);
 
 // fft3.hip: fused frame through the tile-major intermediate; the row pass
 // recomputes wave data and feeds evolve straight into a radix-4/8 first stage;

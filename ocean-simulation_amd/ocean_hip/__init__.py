@@ -62,6 +62,7 @@ EXPORTED_SYMBOLS = (
     "ocean_generate_noise_device", "ocean_read_async", "ocean_readback_status", "ocean_readback_wait", "ocean_readback_release",
     "ocean_host_alloc", "ocean_host_free", "ocean_last_error", "ocean_abi_version", "ocean_set_column_band",
     "ocean_reset_foam", "ocean_sample_world", "ocean_sample_world_device", "ocean_kernel_name",
+    "ocean_set_column_parity",
 )
 
 
@@ -130,6 +131,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "ocean_last_error": ([], ctypes.c_char_p),
         "ocean_abi_version": ([], i),
         "ocean_set_column_band": ([P, i, i], i),
+        "ocean_set_column_parity": ([P, i], i),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -279,6 +281,11 @@ class OceanContext:
         """Restrict the fused step's stores, column transforms and fill to columns
         [x_begin, x_begin + x_count) (one GPU's share of a unit split over several)."""
         _check(self.lib.ocean_set_column_band(self._h, x_begin, x_count), "ocean_set_column_band")
+
+    def set_column_parity(self, parity: int) -> None:
+        """Compute only the columns x = 2m + parity (stored compact at texture column m < N/2):
+        one of two GPUs sharing a unit with no duplicated row transform (ocean.h); -1 = off."""
+        _check(self.lib.ocean_set_column_parity(self._h, parity), "ocean_set_column_parity")
 
     # -- timing ---------------------------------------------------------------
     def set_kernel_timing(self, enable: bool) -> None:

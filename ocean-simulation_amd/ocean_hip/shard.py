@@ -28,13 +28,21 @@ def shard_tiles(total_tiles: int, world: int, rank: int) -> Tuple[int, int]:
 class Shard:
     """One rank's share of a job of `tiles` oceans x C cascades at N^2: global tiles
     [tile0, tile0 + tiles), cascades [casc0, casc0 + cascades) of each, and the column
-    band [x0, x0 + nx) of each of those slices (ocean_set_column_band)."""
+    band [x0, x0 + nx) of each of those slices (ocean_set_column_band) -- or, with
+    parity >= 0, the columns x = 2m + parity (ocean_set_column_parity; x0 = 0, nx = N)."""
     tile0: int
     tiles: int
     casc0: int
     cascades: int
     x0: int
     nx: int
+    parity: int = -1
+
+    def columns(self, n: int):
+        """The global columns this shard computes, in its texture's column order."""
+        if self.parity >= 0:
+            return list(range(self.parity, n, 2))
+        return list(range(self.x0, self.x0 + self.nx))
 
 
 def band_granularity(n: int) -> int:
@@ -42,15 +50,20 @@ def band_granularity(n: int) -> int:
     return min(n, max(16, 8192 // n))
 
 
-def plan_shard(total_tiles: int, n_cascades: int, n: int, world: int, rank: int) -> Shard:
+PARITY_SIZES = (4096,)  # N with a column-parity row pass (ocean_set_column_parity, pass A3P)
+
+
+def plan_shard(total_tiles: int, n_cascades: int, n: int, world: int, rank: int, interleave: bool = True) -> Shard:
     """Split a job over `world` GPUs with no data exchange.
 
     world <= tiles: contiguous tile blocks, every cascade, whole slices (cfg4).
     Otherwise each tile gets s = world / tiles ranks (world a multiple of tiles):
     s <= C: the tile's cascades in contiguous blocks (cfg5 at 2 and 4 GPUs);
-    s > C (s a multiple of C): each cascade split into b = s / C column bands of
-    N / b columns (cfg5 at 8 GPUs: one cascade, half the columns per GPU).  A band
-    rank still runs the full row IFFT of its cascade (rows are needed whole)."""
+    s > C (s a multiple of C): each cascade over b = s / C ranks.  b = 2 at an N with the
+    parity row pass (cfg5 at 8 GPUs) and `interleave`: even / odd columns (rank k of the
+    cascade owns x = 2m + k; each rank transforms its rows at N/2 points instead of
+    duplicating the N-point row transform).  Otherwise b column bands of N / b columns
+    (every band rank runs the full row IFFT of its cascade)."""
     if world < 1 or not 0 <= rank < world:
         raise ValueError("bad world/rank")
     if world <= total_tiles:
@@ -67,6 +80,8 @@ def plan_shard(total_tiles: int, n_cascades: int, n: int, world: int, rank: int)
         raise ValueError(f"{s} ranks per tile over {n_cascades} cascades: must be a multiple")
     b = s // n_cascades
     c, k = divmod(r, b)
+    if b == 2 and interleave and n in PARITY_SIZES:
+        return Shard(tile, 1, c, 1, 0, n, parity=k)
     width = n // b
     if width < band_granularity(n) or width % band_granularity(n):
         raise ValueError(f"{b} column bands of N = {n} are narrower than the band granularity")

@@ -102,15 +102,51 @@ def test_ifft2d_operator_vs_oracle(n):
     ctx.close()
 
 
-@pytest.mark.parametrize("n", [2048, 4096])
-def test_ifft2d_operator_large_vs_numpy(n):
-    ctx = oh.OceanContext(n, 1, 1)
-    rng = np.random.default_rng(1)
-    x = rng.standard_normal((1, n, n, 2)).astype(np.float32)
-    ctx.write(oh.TEX_PLANE0, x[0])
-    ctx.ifft2d(1)
-    got = cplx(ctx.read_all(oh.TEX_PLANE0))
-    assert O.rel_err(got, O.ref64.ifft2d(cplx(x))) <= 2e-6
+@pytest.mark.parametrize("n,C,mask", [(2048, 1, 0b0001), (4096, 4, 0b1111)])
+def test_ifft2d_operator_large_vs_numpy(n, C, mask):
+    """The operator at N = 2048 / 4096 (four-step column passes through the scratch, fft2.hip) on
+    every requested plane of every cascade, against numpy's float64 ifft2 (ref64); 4 x 4096^2 x 4
+    planes is cfg5's whole plane set (2 GiB), one unit-plane per chunk."""
+    ctx = oh.OceanContext(n, C, 1)
+    planes = [p for p in range(4) if mask >> p & 1]
+
+    def slice_data(p, c):
+        return np.random.default_rng(1000 * p + c).standard_normal((n, n, 2)).astype(np.float32)
+
+    for p in planes:
+        for c in range(C):
+            ctx.write(oh.TEX_PLANE0 + p, slice_data(p, c), 0, c)
+    ctx.ifft2d(mask)
+    for p in planes:
+        for c in range(C):
+            got = cplx(ctx.read(oh.TEX_PLANE0 + p, 0, c))
+            want = O.ref64.ifft2d(cplx(slice_data(p, c)[None]))[0]
+            e = O.rel_err(got, want)
+            assert e <= 2e-6, f"plane {p} cascade {c}: {e:.2e}"
+    ctx.close()
+
+
+@pytest.mark.parametrize("chunk_mib", [None, 64])
+def test_ifft2d_operator_2048_vs_oracle(chunk_mib, monkeypatch):
+    """N = 2048 operator against the reference's radix-2 schedule (oracle) on three planes of two
+    cascades (6 unit-planes of 32 MiB): one chunk by default, or 3 chunks of 2 unit-planes at
+    OCEAN_OP_CHUNK_MIB=64; plane 3 untouched."""
+    if chunk_mib:
+        monkeypatch.setenv("OCEAN_OP_CHUNK_MIB", str(chunk_mib))
+    n, C = 2048, 2
+    ctx = oh.OceanContext(n, C, 1)
+    rng = np.random.default_rng(7)
+    planes = [rng.standard_normal((C, n, n, 2)).astype(np.float32) for _ in range(4)]
+    for p in range(4):
+        for c in range(C):
+            ctx.write(oh.TEX_PLANE0 + p, planes[p][c], 0, c)
+    ctx.ifft2d(0b0111)
+    np.testing.assert_array_equal(ctx.read_all(oh.TEX_PLANE3), planes[3])
+    for p in range(3):
+        got = ctx.read_all(oh.TEX_PLANE0 + p)
+        want = O.ifft2d(planes[p])
+        for c in range(C):
+            assert O.rel_err(cplx(got[c]), cplx(want[c])) <= TOL, f"plane {p} cascade {c}"
     ctx.close()
 
 
@@ -711,7 +747,7 @@ def test_split_ocean_shards_bit_identical(n, ncasc, world, flags):
     whole, _ = make_ctx(n, cas, flags=flags)
     shards = []
     for r in range(world):
-        sh = plan_shard(1, ncasc, n, world, r)
+        sh = plan_shard(1, ncasc, n, world, r, interleave=False)
         ctx, _ = make_ctx(n, cas[sh.casc0:sh.casc0 + sh.cascades], flags=flags)
         ctx.set_column_band(sh.x0, sh.nx)
         shards.append((sh, ctx))
@@ -733,6 +769,69 @@ def test_split_ocean_shards_bit_identical(n, ncasc, world, flags):
     whole.close()
     for _, ctx in shards:
         ctx.close()
+
+
+def test_column_parity_shards_vs_oracle():
+    """cfg5 on 8 GPUs as plan_shard splits it: 4 cascades x 4096^2, each cascade's even and odd
+    columns on two ranks (ocean_set_column_parity: pass A3P folds every row to z_b and transforms
+    it at 2048 points), each shard its own context here on one GPU.  Every shard's compact
+    textures (column m = x 2m + b) against the oracle's columns b, b + 2, ... at 1e-5 per cascade
+    and channel, over two frames (foam included); the texture columns m >= N/2 stay untouched; and
+    the shards match the whole single-GPU frame within the same tolerance."""
+    from ocean_hip.shard import plan_shard
+    n, cas = 4096, O.SCENE_CASCADES
+    O.set_threads(min(16, os.cpu_count() or 1))
+    whole, (noise,) = make_ctx(n, cas)
+    shards = []
+    for r in range(8):
+        sh = plan_shard(1, 4, n, 8, r)
+        assert sh.parity == r % 2 and sh.cascades == 1
+        ctx, _ = make_ctx(n, cas[sh.casc0:sh.casc0 + 1])
+        ctx.set_column_parity(sh.parity)
+        shards.append((sh, ctx))
+    oc = O.OracleOcean(n, O.scene_params(), cas, noise)
+    for t in (0.25, 3.0):
+        whole.step(t)
+        for _, ctx in shards:
+            ctx.step(t)
+        disp, deriv, turb = oc.step(t)
+    O.set_threads(1)
+    refs = {oh.TEX_DISP: disp[..., :3], oh.TEX_DERIV: deriv, oh.TEX_TURB: turb}
+    for tex, ref in refs.items():
+        w = whole.read_all(tex)[..., :ref.shape[-1]]
+        for sh, ctx in shards:
+            got = ctx.read(tex)
+            assert not got[:, n // 2:].any(), f"tex {tex} shard {sh}: wrote past the compact half"
+            mine = got[None, :, :n // 2, :ref.shape[-1]]
+            c, b = sh.casc0, sh.parity
+            assert_channels(mine, ref[c:c + 1, :, b::2], what=f"tex {tex} shard {sh} vs oracle")
+            assert_channels(mine, w[c:c + 1, :, b::2], what=f"tex {tex} shard {sh} vs whole frame")
+    whole.close()
+    for _, ctx in shards:
+        ctx.close()
+
+
+def test_column_parity_errors():
+    ctx, _ = make_ctx(1024, O.SCENE_CASCADES[:1])
+    with pytest.raises(oh.OceanError) as e:
+        ctx.set_column_parity(0)
+    assert e.value.code == oh.E_UNSUPPORTED
+    ctx.close()
+    ctx, _ = make_ctx(4096, O.SCENE_CASCADES[:1])
+    with pytest.raises(oh.OceanError) as e:
+        ctx.set_column_parity(2)
+    assert e.value.code == oh.E_INVALID_ARG
+    ctx.set_column_parity(1)
+    a, b = ctx.step_bytes()
+    ctx.set_column_parity(-1)
+    assert ctx.step_bytes()[1] > b  # the whole band again
+    ctx.set_column_parity(0)
+    with pytest.raises(oh.OceanError) as e:
+        ctx.sample_world(np.zeros((1, 3), np.float32))
+    assert e.value.code == oh.E_UNSUPPORTED
+    ctx.set_column_band(0, 4096)  # a band replaces the parity
+    ctx.step(0.5)
+    ctx.close()
 
 
 def test_column_band_narrow_and_restored():

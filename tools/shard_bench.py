@@ -37,7 +37,9 @@ def time_shard(cfg, sh, steps, warmup):
     ctx = oh.OceanContext(n, sh.cascades, sh.tiles, 0)
     ctx.set_params(bench.SCENE_PARAMS, bench.SCENE_CASCADES[sh.casc0:sh.casc0 + sh.cascades])
     ctx.generate_noise(tile_seed(20251121, sh.tile0))
-    if sh.nx != n:
+    if sh.parity >= 0:
+        ctx.set_column_parity(sh.parity)
+    elif sh.nx != n:
         ctx.set_column_band(sh.x0, sh.nx)
     ctx.init_spectrum()
     for f in range(warmup):
@@ -56,7 +58,8 @@ def time_shard(cfg, sh, steps, warmup):
     b_ms, _ = ctx.kernel_stats(1)
     a, b = ctx.step_bytes()
     ctx.close()
-    return {"cascades": [sh.casc0, sh.casc0 + sh.cascades], "columns": [sh.x0, sh.x0 + sh.nx],
+    return {"cascades": [sh.casc0, sh.casc0 + sh.cascades],
+            "columns": f"x = 2m + {sh.parity}" if sh.parity >= 0 else [sh.x0, sh.x0 + sh.nx],
             "tiles": sh.tiles, "ms_per_frame": round(ms, 4),
             "pass_a_ms": round(a_ms / steps, 4), "pass_b_ms": round(b_ms / steps, 4),
             "bytes_per_frame": a + b}
@@ -68,16 +71,17 @@ def main():
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--no-interleave", action="store_true", help="contiguous column bands instead of even / odd")
     ap.add_argument("--all-ranks", action="store_true",
                     help="time every rank (default: one rank per distinct shard shape)")
     args = ap.parse_args()
     cfg = bench.CONFIGS[args.config]
     for w in [int(x) for x in args.worlds.split(",")]:
-        shards = [plan_shard(cfg["tiles"], cfg["cascades"], cfg["n"], w, r) for r in range(w)]
+        shards = [plan_shard(cfg["tiles"], cfg["cascades"], cfg["n"], w, r, not args.no_interleave) for r in range(w)]
         seen, ranks = set(), []
         for r, sh in enumerate(shards):
             # cascade sets differ in spectrum content but not in work: one per (count, band width) shape
-            shape = (sh.tiles, sh.cascades, sh.nx)
+            shape = (sh.tiles, sh.cascades, sh.nx, sh.parity)
             if args.all_ranks or shape not in seen:
                 seen.add(shape)
                 ranks.append(r)
