@@ -446,6 +446,8 @@ def main():
     dom_bytes = B["pass_b" if dom in ("pass_b", "ifft_cols") else "pass_a"]
     if args.unfused:  # unfused row/col launches move 16 B per texel per plane, all planes in one launch
         dom_bytes = n * n * units * 16 * (2 if cfg["disp_only"] else 4)
+        if dom == "ifft_cols" and n >= 2048:  # four-step columns: C1 and C2 each read + write the planes
+            dom_bytes *= 2
     achieved = dom_bytes / (dom_us * 1e-6) / 1e9 if dom_us > 0 else 0.0
 
     kernel_syms = {"pass_a": ctx.kernel_name(0), "pass_b": ctx.kernel_name(1)}

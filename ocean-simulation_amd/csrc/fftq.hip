@@ -104,6 +104,20 @@ __device__ __forceinline__ float2 q4_full(const Planes4& o, const Planes4& om) {
     return make_float2(a2.y + a4.x, -a2.x + a4.y);
 }
 
+// The per-texel factors of texel x of row y that its row mirror N - x shares (nx negated, the same
+// |k|): the phase factor e = exp(i omega t) and 1/|k| as (e.x, e.y, 1/|k|, 0); (1, 0, 1, 0) outside
+// the cascade's band (wave_data's (kx, 1, kz, 0)).  omega = sqrt(g |k|) is correctly rounded as in
+// wave_data (the phase omega t of a large t depends on its last bit); 1/|k| is the hardware
+// reciprocal (1 ulp, inside the fp32 tolerance the three-plane passes are held to).
+template <int N>
+__device__ __forceinline__ float4 mirror_factors(int x, int y, const WaveBand& wb, float g, float time) {
+    const float kx = (float)(x - N / 2) * wb.dk, kz = (float)(y - N / 2) * wb.dk;
+    const float kmag = sqrtf(kx * kx + kz * kz);
+    if (!(kmag >= wb.lo && kmag <= wb.hi)) return make_float4(1.0f, 0.0f, 1.0f, 0.0f);
+    const Phase e = evolve_phase(sqrtf(g * kmag), time);
+    return make_float4(e.ex, e.ey, __builtin_amdgcn_rcpf(kmag), 0.0f);
+}
+
 // Side arrays of unit u (of the chunk the view covers): d0 [N], then srow [N].
 __device__ __forceinline__ float2* q_side(const DevView& v, int u) { return v.qside + (size_t)u * 2 * v.n; }
 
@@ -257,10 +271,18 @@ __global__ __launch_bounds__(N / 4) AQ_WPEU void k_pass_aq(DevView v, float time
 // the Nyquist column / row).  16-wide tile-major intermediate as pass A3.
 // S3: the LDS stages skip the idle fourth sequence slot (its butterflies' lanes only join the
 // stage barriers); row 0 runs srow's input through them in a second pass (one row in N).
-template <int N, bool BAND = false, bool S3 = true, bool EARLY_PF = true>
+// SLIM (N = 1024, A/B): compact twiddles and an LDS image of the three live sequence slots only
+// (S3: slot 3 is never touched; row 0's srow runs through slot 0), 28.6 instead of 43.5 KiB, so four
+// 256-lane workgroups share a CU where the VGPRs allow it.
+// SHARE: texels x and N - x of a row share omega, 1/|k| and the phase factor (mirror_factors): lane
+// j evaluates them for its texels r < 2 and reads r >= 2 from the mirror lane NJ - j (r' = 3 - r;
+// lane 0: r' = 4 - r, and x = N/2 itself) through LDS -- a separate 8 KiB buffer at N = 1024, the
+// (then idle) image at N = 4096 with one more barrier before stage 0.
+template <int N, bool BAND = false, bool S3 = true, bool EARLY_PF = true, bool SLIM = false, bool SHARE = false>
 __global__ __launch_bounds__(N / 4) void k_pass_a3q(DevView v, float time, int total_rows) {
     constexpr int FIRST = 4;
-    using TW = StageTwLds<N, FIRST>;
+    static_assert(!SLIM || S3, "the slim image holds the three live slots of the S3 schedule");
+    using TW = std::conditional_t<SLIM, StageTwCompact<N, FIRST>, StageTwLds<N, FIRST>>;
     using E = Engine<N, 4, false, true, FIRST, TW>;
     constexpr int T = E::THREADS;
     constexpr int R0 = E::R0;
@@ -269,7 +291,12 @@ __global__ __launch_bounds__(N / 4) void k_pass_a3q(DevView v, float time, int t
     constexpr int TILES = N / W;
     constexpr int NSL = N / E::RL;
     static_assert(T == NJ && R0 == 4, "lane j <-> stage-0 butterfly j of each sequence");
-    __shared__ float2 lds[E::LDS_ELEMS];
+    constexpr bool XSEP = SHARE && N <= 1024;  // exchange buffer of its own (else aliased on the image)
+    __shared__ __align__(16) float2 lds[SLIM ? E::LDS_ELEMS / 4 * 3 : E::LDS_ELEMS];
+    __shared__ float4 xsep[XSEP ? 2 * NJ : 1];
+    float4* xch = XSEP ? xsep : reinterpret_cast<float4*>(lds);
+    static_assert(XSEP || !SHARE || 2 * NJ * 16 <= (SLIM ? E::LDS_ELEMS / 4 * 3 : E::LDS_ELEMS) * 8, "xch fits");
+    const int jm = (NJ - (int)threadIdx.x) & (NJ - 1);
     __shared__ float2 twl[TW::kLdsEntries];
     TW::load(twl, v.tw, threadIdx.x, T);
     const float2* tws = TW::table(twl, v.tw);
@@ -292,10 +319,32 @@ __global__ __launch_bounds__(N / 4) void k_pass_a3q(DevView v, float time, int t
         const int u = item / N, y = item % N;
         const WaveBand wb = band[(u + v.c0) % v.C];
         float2 in[4 * R0];  // slot p * R0 + r: sequence p, stage-0 input r
+        float4 own[SHARE ? 2 : 1];
+        if constexpr (SHARE) {
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                own[r] = mirror_factors<N>(j + r * NJ, y, wb, v.gravity, time);
+                xch[r * NJ + j] = own[r];
+            }
+            __syncthreads();
+        }
 #pragma unroll
         for (int r = 0; r < R0; ++r) {
-            const float4 wd = wave_data(j + r * NJ, y, N, wb, v.gravity);
-            const float2 hh = evolve_h(h[r], evolve_phase(wd.w, time));
+            float4 wd;
+            Phase ph;
+            if constexpr (SHARE) {
+                float4 f;
+                const int rp = j0 ? 4 - r : 3 - r;  // the mirror's r' (< 2: exchanged; else evaluated here)
+                if (r < 2) f = own[r];
+                else f = (rp < 2) ? xch[(rp & 1) * NJ + jm] : mirror_factors<N>(j + r * NJ, y, wb, v.gravity, time);
+                wd = make_float4((float)(j + r * NJ - N / 2) * wb.dk, f.z, (float)(y - N / 2) * wb.dk, 0.0f);
+                ph.ex = f.x;
+                ph.ey = f.y;
+            } else {
+                wd = wave_data(j + r * NJ, y, N, wb, v.gravity);
+                ph = evolve_phase(wd.w, time);
+            }
+            const float2 hh = evolve_h(h[r], ph);
             QTex qa, qb;
             in[3 * R0 + r] = make_float2(0.0f, 0.0f);
             if (y != 0 && !(r == 0 && j0)) {
@@ -334,6 +383,7 @@ __global__ __launch_bounds__(N / 4) void k_pass_a3q(DevView v, float time, int t
         } else {
 #pragma unroll
             for (int p = 0; p < 4; ++p) Idft<R0>::run(&in[p * R0]);
+            if constexpr (SHARE && !XSEP) __syncthreads();  // every lane has read the exchange off the image
             // pass 0: Q1..Q3 (sequence slot 3 idle); row 0 only, pass 1: srow's input in slot 0
             for (int ps = 0; ps < (y == 0 ? 2 : 1); ++ps) {
 #pragma unroll
@@ -367,7 +417,14 @@ __global__ __launch_bounds__(N / 4) void k_pass_a3q(DevView v, float time, int t
 // Lane j (N/8 lanes) evolves texels j + r N/8, r < 8; texels r and r + 4 give z_b[j + r N/8], r < 4:
 // stage-0 butterfly j of the N/2-point plan with first radix 4 (the engine of pass A3Q at N/2).
 // Outputs m < N/2 go to intermediate column m (compact); srow likewise.  d0 is per row (texel 0).
-template <int N, bool EARLY_PF = A3P_EARLY_PF>
+// SHARE: texel x and its row mirror N - x have the same |k| (nx negated), so the same 1/|k|, omega
+// and phase factor e = exp(i omega t): lane j computes them for its texels r < 4 and reads those of
+// r >= 4 from the lane that owns the mirrors (512 - j, r' = 7 - r; lane 0: r' = 8 - r, and x = N/2
+// itself) through an LDS exchange -- half the square roots, divisions and sincos of the evolve (pass
+// A3P issues ~190 VALU per texel against ~175 for pass AQ's full-length transforms, SQ counters).
+// The exchanged 1/|k| is a hardware reciprocal (1 ulp; omega stays correctly rounded, the phase
+// omega t of large t depends on it), and the srow sequence is formed on row 0 only.
+template <int N, bool EARLY_PF = A3P_EARLY_PF, bool SHARE = true>
 __global__ __launch_bounds__(N / 8) A3P_WPEU void k_pass_a3p(DevView v, float time, int total_rows) {
     constexpr int H = N / 2;  // transform length
     constexpr int FIRST = 4;
@@ -382,12 +439,14 @@ __global__ __launch_bounds__(N / 8) A3P_WPEU void k_pass_a3p(DevView v, float ti
     static_assert(T == NJ && R0 == 4 && T == N / 8, "lane j <-> stage-0 butterfly j of each sequence");
     __shared__ float2 lds[E::LDS_ELEMS];
     __shared__ float2 twl[TW::kLdsEntries];
+    __shared__ float4 xch[SHARE ? R0 * NJ : 1];  // (e.x, e.y, 1/|k|, -) of texel j + r NJ at [r][j]
     TW::load(twl, v.tw, threadIdx.x, T);
     const float2* tws = twl;
     __shared__ WaveBand band[kMaxCascades];
     if ((int)threadIdx.x < v.C) band[threadIdx.x] = wave_band(v.casc + threadIdx.x * 5);
     const int j = (int)threadIdx.x;
     const bool j0 = (j == 0);
+    const int jm = (NJ - j) & (NJ - 1);  // lane of the mirrors (r' = 7 - r; lane 0: 8 - r)
     const int par = v.xpar;
     const float sgn = par ? -1.0f : 1.0f;
     float4 h[2 * R0];
@@ -400,6 +459,15 @@ __global__ __launch_bounds__(N / 8) A3P_WPEU void k_pass_a3p(DevView v, float ti
     float2 zt[R0];
 #pragma unroll
     for (int r = 0; r < R0; ++r) zt[r] = par ? v.tw[j + r * NJ] : make_float2(1.0f, 0.0f);
+    // the shared per-texel factors of texel x of row y: (e.x, e.y, 1/|k|)
+    auto factors = [&](int x, int y, const WaveBand& wb) {
+        const int nx = x - N / 2, nz = y - N / 2;
+        const float kx = (float)nx * wb.dk, kz = (float)nz * wb.dk;
+        const float kmag = sqrtf(kx * kx + kz * kz);
+        if (!(kmag >= wb.lo && kmag <= wb.hi)) return make_float4(1.0f, 0.0f, 1.0f, 0.0f);
+        const Phase e = evolve_phase(sqrtf(v.gravity * kmag), time);
+        return make_float4(e.ex, e.ey, __builtin_amdgcn_rcpf(kmag), 0.0f);
+    };
     int item = (gridDim.x % 8 == 0) ? (int)(blockIdx.x % 8) * (int)(gridDim.x / 8) + (int)blockIdx.x / 8
                                     : (int)blockIdx.x;
     if (item < total_rows) load(item, h);
@@ -407,6 +475,15 @@ __global__ __launch_bounds__(N / 8) A3P_WPEU void k_pass_a3p(DevView v, float ti
     for (; item < total_rows; item += gridDim.x) {
         const int u = item / N, y = item % N;
         const WaveBand wb = band[(u + v.c0) % v.C];
+        float4 own[SHARE ? R0 : 1];
+        if constexpr (SHARE) {
+#pragma unroll
+            for (int r = 0; r < R0; ++r) {
+                own[r] = factors(j + r * NJ, y, wb);
+                xch[r * NJ + j] = own[r];
+            }
+            __syncthreads();
+        }
         float2 in[4 * R0];  // slot p * R0 + r: sequence p, stage-0 input r (z_b[j + r NJ])
 #pragma unroll
         for (int r = 0; r < R0; ++r) {
@@ -414,8 +491,25 @@ __global__ __launch_bounds__(N / 8) A3P_WPEU void k_pass_a3p(DevView v, float ti
 #pragma unroll
             for (int hi = 0; hi < 2; ++hi) {
                 const int rr = r + hi * R0;
-                const float4 wd = wave_data(j + rr * NJ, y, N, wb, v.gravity);
-                const float2 hh = evolve_h(h[rr], evolve_phase(wd.w, time));
+                float4 wd;
+                Phase ph;
+                if constexpr (SHARE) {
+                    float4 f;
+                    if (hi == 0) {
+                        f = own[r];
+                    } else {
+                        const int rp = j0 ? 2 * R0 - rr : 2 * R0 - 1 - rr;  // the mirror's r' (< 4, or 4 on lane 0)
+                        f = (rp < R0) ? xch[(rp & (R0 - 1)) * NJ + jm] : factors(j + rr * NJ, y, wb);
+                    }
+                    const float kx = (float)(j + rr * NJ - N / 2) * wb.dk, kz = (float)(y - N / 2) * wb.dk;
+                    wd = make_float4(kx, f.z, kz, 0.0f);
+                    ph.ex = f.x;
+                    ph.ey = f.y;
+                } else {
+                    wd = wave_data(j + rr * NJ, y, N, wb, v.gravity);
+                    ph = evolve_phase(wd.w, time);
+                }
+                const float2 hh = evolve_h(h[rr], ph);
                 QTex qa, qb;
                 qv[hi][3] = make_float2(0.0f, 0.0f);
                 if (y != 0 && !(rr == 0 && j0)) {
@@ -432,6 +526,10 @@ __global__ __launch_bounds__(N / 8) A3P_WPEU void k_pass_a3p(DevView v, float ti
             }
 #pragma unroll
             for (int p = 0; p < 4; ++p) {
+                if (SHARE && p == 3 && y != 0) {  // srow's sequence exists on row 0 only
+                    in[p * R0 + r] = make_float2(0.0f, 0.0f);
+                    continue;
+                }
                 const float2 zs = make_float2(qv[0][p].x + sgn * qv[1][p].x, qv[0][p].y + sgn * qv[1][p].y);
                 in[p * R0 + r] = par ? cmul(zs, zt[r]) : zs;
             }
@@ -643,21 +741,23 @@ hipError_t go_aq(const DevView& v, float t, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <int N, bool BAND = false, bool S3 = true, bool PF = true>
+template <int N, bool BAND = false, bool S3 = true, bool PF = true, bool SLIM = false, bool SHARE = false>
 hipError_t go_a3q(const DevView& v, float t, hipStream_t s) {
-    if constexpr (S3 && PF) {
+    if constexpr (S3 && PF && !SLIM && !SHARE) {
         static const int s3 = env_int_q("OCEAN_A3Q_S3", 1);  // 0: the four-sequence stages on every row (A/B)
         static const int pf = env_int_q("OCEAN_A3Q_PF", 1);  // 0: next row's h0 loaded after the stages (A/B)
+        static const int sh = env_int_q("OCEAN_A3Q_SHARE", 0);  // 1: mirror factors exchanged (A/B)
         if (!s3) return go_a3q<N, BAND, false, PF>(v, t, s);
         if (!pf) return go_a3q<N, BAND, S3, false>(v, t, s);
+        if (sh) return go_a3q<N, BAND, S3, PF, false, true>(v, t, s);
     }
     if constexpr (!BAND) {
-        if (v.nx != N) return go_a3q<N, true, S3, PF>(v, t, s);
+        if (v.nx != N) return go_a3q<N, true, S3, PF, SLIM, SHARE>(v, t, s);
     }
     constexpr int T = N / 4;
     const int total = v.units * N;
-    const int g = grid_q(k_pass_a3q<N, BAND, S3, PF>, T, total);
-    launch((k_pass_a3q<N, BAND, S3, PF>), dim3(g), dim3(T), 0, s, v, t, total);
+    const int g = grid_q(k_pass_a3q<N, BAND, S3, PF, SLIM, SHARE>, T, total);
+    launch((k_pass_a3q<N, BAND, S3, PF, SLIM, SHARE>), dim3(g), dim3(T), 0, s, v, t, total);
     return hipGetLastError();
 }
 
@@ -692,10 +792,26 @@ hipError_t launch_pass_a_q(const DevView& v, float t, hipStream_t s) {
         if (v.n != 4096 || v.x0 != 0 || v.nx != v.n / 2) return hipErrorInvalidValue;
         constexpr int T = 4096 / 8;
         const int total = v.units * 4096;
+        static const int share = env_int_q("OCEAN_A3P_SHARE", 1);  // 0: every texel evaluates its own factors (A/B)
+        if (!share) {
+            const int g = grid_q(k_pass_a3p<4096, A3P_EARLY_PF, false>, T, total);
+            launch((k_pass_a3p<4096, A3P_EARLY_PF, false>), dim3(g), dim3(T), 0, s, v, t, total);
+            return hipGetLastError();
+        }
         const int g = grid_q(k_pass_a3p<4096>, T, total);
         launch((k_pass_a3p<4096>), dim3(g), dim3(T), 0, s, v, t, total);
         return hipGetLastError();
     }
+    // OCEAN_AQ_ROWS=1: the one-row-per-item pass A3Q at N = 1024 (full h0, 16 B per texel) instead of the
+    // mirror-pair pass AQ (h0k, 8 B per texel); A/B
+    static const int aq_rows = env_int_q("OCEAN_AQ_ROWS", 0);
+    static const int aq_rows_pf = env_int_q("OCEAN_AQ_ROWS_PF", 1);
+    if (aq_rows == 1 && v.n == 1024) return aq_rows_pf ? go_a3q<1024>(v, t, s) : go_a3q<1024, false, true, false>(v, t, s);
+    if (aq_rows == 2 && v.n == 1024)  // slim image
+        return aq_rows_pf ? go_a3q<1024, false, true, true, true>(v, t, s) : go_a3q<1024, false, true, false, true>(v, t, s);
+    if (aq_rows == 3 && v.n == 1024)  // slim image, mirror factors exchanged
+        return aq_rows_pf ? go_a3q<1024, false, true, true, true, true>(v, t, s)
+                          : go_a3q<1024, false, true, false, true, true>(v, t, s);
     switch (v.n) {
         case 512: return v.h0k ? go_aq<512>(v, t, s) : hipErrorInvalidValue;
         case 1024: return v.h0k ? go_aq<1024>(v, t, s) : hipErrorInvalidValue;

@@ -938,11 +938,16 @@ def test_launch_variants_bit_identical(tmp_path, var, n, ncasc, flags):
 
 @pytest.mark.parametrize("var,val,n,ncasc,flags", [("OCEAN_B8", "0", 512, 1, oh.F_DISPLACEMENT_ONLY),
                                                    ("OCEAN_B8", "0", 512, 2, oh.F_DISPLACEMENT_ONLY),
-                                                   ("OCEAN_A8", "0", 512, 1, oh.F_DISPLACEMENT_ONLY)])
+                                                   ("OCEAN_A8", "0", 512, 1, oh.F_DISPLACEMENT_ONLY),
+                                                   ("OCEAN_AQ_ROWS", "3", 1024, 4, 0),
+                                                   ("OCEAN_AQ_ROWS", "2", 1024, 2, 0),
+                                                   ("OCEAN_A3Q_SHARE", "1", 4096, 1, 0)])
 def test_launch_variants_vs_oracle(tmp_path, var, val, n, ncasc, flags):
-    """Variants whose radix order differs from the default's (OCEAN_B8=0: pass B's radix-16 engine
-    instead of pass B8's radix 8 x 8 x 8; OCEAN_A8=0: pass A4's radix-16 engine), so they match within
-    the fp32 tolerance, not bit for bit: each runs in its own process (knobs are read once per
+    """Variants whose radix order or arithmetic differs from the default's (OCEAN_B8=0: pass B's radix-16
+    engine instead of pass B8's radix 8 x 8 x 8; OCEAN_A8=0: pass A4's radix-16 engine; OCEAN_AQ_ROWS:
+    the one-row three-plane pass at 1024 instead of the mirror-pair one, 2 = slim image, 3 = also the
+    mirror factors exchanged; OCEAN_A3Q_SHARE=1: the exchanged factors at 4096, reciprocal 1/|k|), so
+    they match within the fp32 tolerance, not bit for bit: each runs in its own process (knobs are read once per
     process), and its third frame (t = 250 s, foam over all three) is checked against the radix-2 oracle at 1e-5 norm-relative per channel and cascade."""
     import subprocess
     import sys
