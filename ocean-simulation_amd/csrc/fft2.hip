@@ -345,16 +345,23 @@ struct Cols2 {
 // allocation: plane p of unit u is unit-plane p * U + u), through `scratch` (>= ups unit-planes).
 template <int N>
 struct Op4 {
+    template <int B>
+    static hipError_t rows_to(const DevView* v, float2* planes, int ups, float2* scratch, hipStream_t s) {
+        constexpr int T = B * N / kElems;
+        const int total = ups * N;
+        const int items = (total + B - 1) / B;
+        const int g = persistent_grid(k_rows2<N, B>, T, items);
+        launch((k_rows2<N, B>), dim3(g), dim3(T), 0, s, (const float2*)planes, scratch, total, v->tw);
+        return hipGetLastError();
+    }
     static hipError_t go(const DevView* v, float2* planes, int ups, float2* scratch, int part, hipStream_t s) {
         if constexpr (N < 2048) {
             return hipErrorInvalidValue;
         } else {
             if (part == 0) {  // rows: planes -> scratch
-                constexpr int B = rows_per_item(N), T = B * N / kElems;
-                const int total = ups * N;
-                const int items = (total + B - 1) / B;
-                const int g = persistent_grid(k_rows2<N, B>, T, items);
-                launch((k_rows2<N, B>), dim3(g), dim3(T), 0, s, (const float2*)planes, scratch, total, v->tw);
+                static const int rb = std::getenv("OCEAN_OP_ROWS_B") ? std::atoi(std::getenv("OCEAN_OP_ROWS_B")) : 1;
+                if (rb == 2) return rows_to<2>(v, planes, ups, scratch, s);  // A/B: two rows per workgroup
+                return rows_to<rows_per_item(N)>(v, planes, ups, scratch, s);
             } else if (part == 1) {  // C1 in place on the scratch
                 constexpr int T = kOpSeq * (N / kOpL1) / kElems;
                 const int items = ups * (N / kOpW) * (kOpL1 / kOpBlk);

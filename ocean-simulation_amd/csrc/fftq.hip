@@ -29,6 +29,9 @@
 #ifndef OCEAN_AQ_CTW
 #define OCEAN_AQ_CTW 0  // 1: compact LDS twiddle tables in pass AQ (37.4 instead of 43.5 KiB; A/B builds)
 #endif
+#ifndef OCEAN_AQ_RCP
+#define OCEAN_AQ_RCP 0  // 1: pass AQ takes 1/|k| from the hardware reciprocal (A/B builds)
+#endif
 #ifndef AQ_SKIP
 #define AQ_SKIP 1  // pass AQ's idle pass-1 waves skip the stages (A/B builds)
 #endif
@@ -191,8 +194,15 @@ __global__ __launch_bounds__(N / 4) AQ_WPEU void k_pass_aq(DevView v, float time
             float2 mir[3][R0];
 #pragma unroll
             for (int r = 0; r < R0; ++r) {
+#if OCEAN_AQ_RCP
+                // hardware reciprocal for 1/|k| (mirror_factors); omega and the phase as wave_data's
+                const float4 f = mirror_factors<N>(j + r * NJ, y1, wb, v.gravity, time);
+                const float4 wd = make_float4((float)(j + r * NJ - N / 2) * wb.dk, f.z, (float)(y1 - N / 2) * wb.dk, 0.0f);
+                const float2 h = evolve_h(make_float4(A[r].x, A[r].y, B[r].x, -B[r].y), Phase{f.x, f.y});
+#else
                 const float4 wd = wave_data(j + r * NJ, y1, N, wb, v.gravity);
                 const float2 h = evolve_h(make_float4(A[r].x, A[r].y, B[r].x, -B[r].y), evolve_phase(wd.w, time));
+#endif
                 QTex qa, qb;
                 if (y1 != 0 && !(r == 0 && j0)) {
                     q_fast(h, wd, qa, qb);
