@@ -304,8 +304,9 @@ def cpu_baseline(cfg, frames=3):
     return {"value": per_tile, "unit": "frames/s", "cores": 1, "kind": "port",
             "sample": f"median of {frames} frames after 1 warm-up, 1 ocean of {C} x {n_s}^2 "
                       f"{'(scaled x%.2f to %d^2) ' % (scale, n) if scale != 1 else ''}"
-                      f"on 1 host core; C port of the reference path (oracle/ocean_oracle.c); "
-                      f"the C# scalar baseline of north_star needs dotnet, absent on this image",
+                      f"on 1 host core; C port of the reference path (oracle/ocean_oracle.c), standing in for "
+                      f"the C# scalar baseline of north_star (ocean-simulation_amd/csharp/CpuOcean.cs, "
+                      f"compile-ready, same op order) because dotnet is absent on this image",
             "multicore": multi}
 
 

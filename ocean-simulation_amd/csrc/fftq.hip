@@ -30,7 +30,10 @@
 #define OCEAN_AQ_CTW 0  // 1: compact LDS twiddle tables in pass AQ (37.4 instead of 43.5 KiB; A/B builds)
 #endif
 #ifndef OCEAN_AQ_RCP
-#define OCEAN_AQ_RCP 0  // 1: pass AQ takes 1/|k| from the hardware reciprocal (A/B builds)
+#define OCEAN_AQ_RCP 1  // pass AQ takes 1/|k| from the hardware reciprocal: cfg3 pass A 29.8 -> 28.6-29.3 us
+#endif
+#ifndef OCEAN_AQ_SHARE
+#define OCEAN_AQ_SHARE 0  // 1: pass AQ also exchanges the in-row mirror texels' factors through LDS (A/B builds)
 #endif
 #ifndef AQ_SKIP
 #define AQ_SKIP 1  // pass AQ's idle pass-1 waves skip the stages (A/B builds)
@@ -149,6 +152,9 @@ __global__ __launch_bounds__(N / 4) AQ_WPEU void k_pass_aq(DevView v, float time
     const float2* tws = TW::table(twl, v.tw);
     __shared__ WaveBand band[kMaxCascades];
     if ((int)threadIdx.x < v.C) band[threadIdx.x] = wave_band(v.casc + threadIdx.x * 5);
+#if OCEAN_AQ_SHARE
+    __shared__ float4 xch[2 * NJ];  // (e.x, e.y, 1/|k|, -) of texel j + r NJ of row y1 at [r][j], r < 2
+#endif
     const int j = (int)threadIdx.x;
     const int jm = (NJ - j) & (NJ - 1);
     const bool j0 = (j == 0);
@@ -188,13 +194,29 @@ __global__ __launch_bounds__(N / 4) AQ_WPEU void k_pass_aq(DevView v, float time
         rows_of(it, u, y1, y2);
         const WaveBand wb = band[(u + v.c0) % v.C];
         const bool self = (y1 == y2);
+#if OCEAN_AQ_SHARE
+        float4 own[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            own[r] = mirror_factors<N>(j + r * NJ, y1, wb, v.gravity, time);
+            xch[r * NJ + j] = own[r];
+        }
+        __syncthreads();
+#endif
         // after stage 0: g = (Q1 y1, Q1 y2, Q2 y1, Q2 y2, Q3 y1, Q3 y2 | row 0: srow's input)
         float2 g[6][R0];
         {
             float2 mir[3][R0];
 #pragma unroll
             for (int r = 0; r < R0; ++r) {
-#if OCEAN_AQ_RCP
+#if OCEAN_AQ_SHARE
+                // texels x and N - x of row y1 share the factors: r < 2 evaluated here, r >= 2 exchanged
+                const int rp = j0 ? R0 - r : R0 - 1 - r;
+                const float4 f = (r < 2) ? own[r] : (rp < 2) ? xch[(rp & 1) * NJ + jm]
+                                                             : mirror_factors<N>(j + r * NJ, y1, wb, v.gravity, time);
+                const float4 wd = make_float4((float)(j + r * NJ - N / 2) * wb.dk, f.z, (float)(y1 - N / 2) * wb.dk, 0.0f);
+                const float2 h = evolve_h(make_float4(A[r].x, A[r].y, B[r].x, -B[r].y), Phase{f.x, f.y});
+#elif OCEAN_AQ_RCP
                 // hardware reciprocal for 1/|k| (mirror_factors); omega and the phase as wave_data's
                 const float4 f = mirror_factors<N>(j + r * NJ, y1, wb, v.gravity, time);
                 const float4 wd = make_float4((float)(j + r * NJ - N / 2) * wb.dk, f.z, (float)(y1 - N / 2) * wb.dk, 0.0f);

@@ -55,6 +55,10 @@ const void*& last_kernel() {
     thread_local const void* slot = nullptr;
     return slot;
 }
+int& last_kernel_nargs() {
+    thread_local int n = 0;
+    return n;
+}
 
 namespace {
 std::mutex g_occ_mu;
@@ -185,6 +189,19 @@ struct ocean_ctx {
     double kind_ms[3] = {0, 0, 0};
     long long kind_count[3] = {0, 0, 0};
     const void* kind_kernel[3] = {nullptr, nullptr, nullptr};  // last kernel launched per kind (ocean_kernel_name)
+    // OCEAN_GRAPH=1: ocean_step replays one captured hipGraph of the fused frame, the time argument of
+    // its pass-A kernel nodes updated per frame
+    int graph_mode = 0;
+    bool capturing = false;
+    std::vector<std::pair<const void*, int>> captured_time_kernels;  // (kernel, argument count), kind 0
+    struct FrameGraph {
+        hipGraph_t g = nullptr;
+        hipGraphExec_t exec = nullptr;
+        std::vector<std::pair<hipGraphNode_t, int>> tnodes;  // pass-A kernel nodes, argument count
+        int x0 = -1, nx = -1, par = -2;
+        bool q = false;
+    } fg;
+    bool graph_stale = false;  // the captured frame's arguments changed (init_spectrum, uploads)
     static constexpr size_t kMaxPending = 2048;  // timed launches held before folding into kind_ms
 
     size_t texels() const { return (size_t)n * n; }
@@ -281,7 +298,11 @@ int timed(ocean_ctx* ctx, int kind, F&& launch, const char* what) {
     ocean::last_kernel() = nullptr;
     if (!ctx->timing) {
         const hipError_t e = launch();
-        if (ocean::last_kernel()) ctx->kind_kernel[kind] = ocean::last_kernel();
+        if (ocean::last_kernel()) {
+            ctx->kind_kernel[kind] = ocean::last_kernel();
+            if (ctx->capturing && kind == 0)
+                ctx->captured_time_kernels.emplace_back(ocean::last_kernel(), ocean::last_kernel_nargs());
+        }
         return e == hipSuccess ? OCEAN_OK : hip_fail(e, what);
     }
     if (ctx->pending.size() >= ocean_ctx::kMaxPending) {
@@ -350,6 +371,8 @@ void free_all(ocean_ctx* c) {
         (void)hipEventDestroy(t.b);
     }
     for (auto e : c->event_pool) (void)hipEventDestroy(e);
+    if (c->fg.exec) (void)hipGraphExecDestroy(c->fg.exec);
+    if (c->fg.g) (void)hipGraphDestroy(c->fg.g);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     if (c->stream) (void)hipStreamDestroy(c->stream);
 }
@@ -409,6 +432,7 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
     if (const char* km = std::getenv("OCEAN_CHUNK_MIN")) c->chunk_min = std::max(1, std::atoi(km));
     if (const char* kr = std::getenv("OCEAN_CHUNK_REUSE")) c->chunk_reuse = std::atoi(kr);
     if (const char* kf = std::getenv("OCEAN_OP_FOUR_STEP")) c->op_four_step = std::atoi(kf);
+    if (const char* kg = std::getenv("OCEAN_GRAPH")) c->graph_mode = std::atoi(kg);
     if (const char* ko = std::getenv("OCEAN_OP_CHUNK_MIB")) c->op_chunk_mib = std::max(0L, std::atol(ko));
     // Width of the fused path's column tiles.  With fewer tiles than CUs (one 512^2
     // cascade: 32 tiles of 16 columns) pass B ran on an eighth of the chip, so small
@@ -588,6 +612,7 @@ int ocean_init_spectrum(ocean_ctx* ctx) {
     ctx->spectrum_ready = true;
     ctx->h0k_valid = ctx->h0k != nullptr;
     ctx->h0_conj = true;
+    ctx->graph_stale = true;  // the kernels' DevView argument carries the active gravity
     return OCEAN_OK;
 }
 
@@ -675,6 +700,77 @@ int ocean_fill(ocean_ctx* ctx) {
 
 namespace {
 int step_fused(ocean_ctx* ctx, float time);
+bool use_q(const ocean_ctx* ctx);
+
+void drop_graph(ocean_ctx* ctx) {
+    if (ctx->fg.exec) (void)hipGraphExecDestroy(ctx->fg.exec);
+    if (ctx->fg.g) (void)hipGraphDestroy(ctx->fg.g);
+    ctx->fg = ocean_ctx::FrameGraph{};
+}
+
+// The fused frame as one hipGraph (OCEAN_GRAPH=1): captured from step_fused on the first frame (and
+// again when the schedule changes: column band / parity, three-plane or four-plane), then replayed
+// with the time argument (argument 1 of every pass-A kernel) set on its kernel nodes per frame.
+int step_graph(ocean_ctx* ctx, float time) {
+    auto& fg = ctx->fg;
+    const bool q = use_q(ctx);
+    if (!fg.exec || ctx->graph_stale || fg.x0 != ctx->band_x0 || fg.nx != ctx->band_nx || fg.par != ctx->col_par ||
+        fg.q != q) {
+        drop_graph(ctx);
+        ctx->graph_stale = false;
+        ctx->captured_time_kernels.clear();
+        OCEAN_HIP(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+        ctx->capturing = true;
+        const int r = step_fused(ctx, time);
+        ctx->capturing = false;
+        hipGraph_t g = nullptr;
+        const hipError_t ec = hipStreamEndCapture(ctx->stream, &g);
+        if (r != OCEAN_OK) {
+            if (g) (void)hipGraphDestroy(g);
+            return r;
+        }
+        if (ec != hipSuccess) return hip_fail(ec, "hipStreamEndCapture");
+        fg.g = g;
+        OCEAN_HIP(hipGraphInstantiate(&fg.exec, g, nullptr, nullptr, 0));
+        size_t n = 0;
+        OCEAN_HIP(hipGraphGetNodes(g, nullptr, &n));
+        std::vector<hipGraphNode_t> nodes(n);
+        OCEAN_HIP(hipGraphGetNodes(g, nodes.data(), &n));
+        for (hipGraphNode_t nd : nodes) {
+            hipGraphNodeType t;
+            OCEAN_HIP(hipGraphNodeGetType(nd, &t));
+            if (t != hipGraphNodeTypeKernel) continue;
+            hipKernelNodeParams p{};
+            OCEAN_HIP(hipGraphKernelNodeGetParams(nd, &p));
+            for (const auto& k : ctx->captured_time_kernels)
+                if (k.first == p.func) {
+                    if (!p.kernelParams || *static_cast<const float*>(p.kernelParams[1]) != time) {
+                        drop_graph(ctx);
+                        return fail(OCEAN_E_DEVICE, "captured frame graph: the pass-A time argument was not found");
+                    }
+                    fg.tnodes.emplace_back(nd, k.second);
+                    break;
+                }
+        }
+        fg.x0 = ctx->band_x0;
+        fg.nx = ctx->band_nx;
+        fg.par = ctx->col_par;
+        fg.q = q;
+    } else {
+        for (const auto& tn : fg.tnodes) {
+            hipKernelNodeParams p{};
+            OCEAN_HIP(hipGraphKernelNodeGetParams(tn.first, &p));
+            void* args[8];
+            for (int i = 0; i < tn.second && i < 8; ++i) args[i] = p.kernelParams[i];
+            float t = time;
+            args[1] = &t;
+            p.kernelParams = args;
+            OCEAN_HIP(hipGraphExecKernelNodeSetParams(fg.exec, tn.first, &p));
+        }
+    }
+    OCEAN_HIP(hipGraphLaunch(fg.exec, ctx->stream));
+    return OCEAN_OK;
+}
 
 // GenerateMips (WaterBody.cs:191-192) when the context has mip chains.
 int generate_mips(ocean_ctx* ctx) {
@@ -691,6 +787,10 @@ int ocean_step(ocean_ctx* ctx, float time) {
         if (int r = ocean_evolve(ctx, time)) return r;
         if (int r = ocean_ifft2d(ctx, (1 << ctx->P) - 1)) return r;
         if (int r = ocean_fill(ctx)) return r;
+        return generate_mips(ctx);
+    }
+    if (ctx->graph_mode && !ctx->timing) {
+        if (int r = step_graph(ctx, time)) return r;
         return generate_mips(ctx);
     }
     if (int r = step_fused(ctx, time)) return r;
@@ -980,6 +1080,7 @@ int ocean_write(ocean_ctx* ctx, int texture, int tile, int cascade, const void* 
     if (texture == OCEAN_TEX_H0) {  // the v3 row pass reads h0 (.zw included); the three-plane frame
         ctx->h0k_valid = false;     // needs .zw = conj h0(-k), which an upload need not keep
         ctx->h0_conj = false;
+        ctx->graph_stale = true;
     }
     if (texture == OCEAN_TEX_TURB) {  // foam state follows the uploaded TURB.x (resume)
         const ocean::DevView v = ctx->view();

@@ -20,12 +20,15 @@ struct LaunchEvents {
     bool launched;
 };
 LaunchEvents*& launch_events();  // thread-local slot, ocean_abi.cpp
-// Host pointer of the kernel this thread launched last (ocean_kernel_name reports its symbol).
+// Host pointer and argument count of the kernel this thread launched last (ocean_kernel_name reports
+// its symbol; the captured frame graph finds its time argument by it).
 const void*& last_kernel();  // thread-local slot, ocean_abi.cpp
+int& last_kernel_nargs();
 
 template <class F, class... Args>
 inline void launch(F kernel, dim3 grid, dim3 block, uint32_t shmem, hipStream_t s, Args... args) {
     last_kernel() = (const void*)kernel;
+    last_kernel_nargs() = (int)sizeof...(Args);
     LaunchEvents* e = launch_events();
     hipExtLaunchKernelGGL(kernel, grid, block, shmem, s, e && !e->launched ? e->start : nullptr,
                           e ? e->stop : nullptr, 0, args...);

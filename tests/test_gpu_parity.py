@@ -910,11 +910,14 @@ ctx.close()
 @pytest.mark.parametrize("var,n,ncasc,flags", [("OCEAN_B2D", 512, 1, oh.F_DISPLACEMENT_ONLY),
                                                ("OCEAN_B2D", 256, 2, oh.F_DISPLACEMENT_ONLY),
                                                ("OCEAN_A3Q_S3", 4096, 1, 0), ("OCEAN_A3Q_PF", 4096, 1, 0),
-                                               ("OCEAN_A3_EPF", 4096, 1, oh.F_DISPLACEMENT_ONLY)])
+                                               ("OCEAN_A3_EPF", 4096, 1, oh.F_DISPLACEMENT_ONLY),
+                                               ("OCEAN_GRAPH", 512, 1, oh.F_DISPLACEMENT_ONLY),
+                                               ("OCEAN_GRAPH", 1024, 4, 0)])
 def test_launch_variants_bit_identical(tmp_path, var, n, ncasc, flags):
     """Schedule knobs read once per process at first launch (environment knobs):
     side-by-side vs sequential pass-B planes (B2D), pass A3Q's idle-slot skip (S3) and early h0
-    prefetch (PF), pass A3's early prefetch at N = 4096 (EPF).  Each variant runs in its own
+    prefetch (PF), pass A3's early prefetch at N = 4096 (EPF), the frame replayed as one captured
+    hipGraph with its time argument updated per frame (GRAPH).  Each variant runs in its own
     process; 3 frames incl. foam, every output bit equal."""
     import subprocess
     import sys
