@@ -200,7 +200,7 @@ def ifft_measure(ctx, reps, csv_name, pmc_config):
     algorithmic bytes 32 B per texel per plane (two passes x read + write), the symbols of the row
     and column kernels that ran, and the committed rocprofv3 / PMC records of exactly those symbols."""
     n, units = ctx.n, ctx.C * ctx.T
-    for _ in range(3):  # first launches load the row/column code objects: keep them out of the timing
+    for _ in range(5):  # first launches load the row/column code objects: keep them out of the timing
         ctx.ifft2d(0b1111)
     ctx.synchronize()
     s0 = time.perf_counter()  # wall region: no events
@@ -245,7 +245,7 @@ def ifft_measure(ctx, reps, csv_name, pmc_config):
             "symbols": syms, "rocprof": rocprof, "traffic": traffic}
 
 
-def ifft_beyond_cache(reps=20):
+def ifft_beyond_cache(reps=50):
     """The operator IFFT at N = 1024 on a plane set twice the 256 MiB Infinity Cache: 4 tiles x 4
     cascades x 4 planes = 512 MiB, so the operator's bytes cannot all be
     cache-resident between its launches."""
