@@ -603,6 +603,182 @@ __global__ __launch_bounds__(N / 8) A3P_WPEU void k_pass_a3p(DevView v, float ti
     }
 }
 
+// Pass A3PP (N = 4096, column parity b, ocean_set_column_parity; OCEAN_A3P_PAIR=1): pass A3P on
+// mirror-pair rows, as pass AQ pairs them.  Item i of a unit is row y1 = i with y2 = (N - i) % N;
+// lane j loads h0k of texels x_r = j + r N/8 (r < 8) of row y1 and of their mirrors N - x_r in row
+// y2 (8 B per texel instead of pass A3P's 16: h(-k) = conj h(k) from the pair), evaluates the
+// shared factors once per texel pair (and, through the LDS exchange, once per four texels: x and
+// N - x of row y1 share them too), and folds z_b for both rows: row y1 at stage-0 butterfly j, row
+// y2 at butterfly jm = (N/8 - j) % (N/8).  Eight sequence slots, two radix-16 butterflies per lane
+// per LDS stage: 0-2 Q1..Q3 of row y1, 3-5 of row y2, 6 row 0's srow, 7 idle.  The self-mirror rows
+// 0 and N/2 run the same code; their y2 slots duplicate y1 and are not stored.
+template <int N, bool EARLY_PF = true>
+__global__ __launch_bounds__(N / 8) void k_pass_a3pp(DevView v, float time, int items) {
+    constexpr int H = N / 2;  // transform length
+    constexpr int FIRST = 4;
+    using TW = StageTwCompactSub<H, N, FIRST>;
+    using E = Engine<H, 8, false, true, FIRST, TW, 32>;
+    constexpr int T = E::THREADS;
+    constexpr int R0 = E::R0;
+    constexpr int NJ = H / R0;  // lanes = texel stride
+    constexpr int W = inter_w(N);
+    constexpr int TILES = N / W;
+    constexpr int NSL = H / E::RL;
+    constexpr int IPU = N / 2 + 1;  // items per unit
+    static_assert(T == NJ && R0 == 4 && T == N / 8, "lane j <-> stage-0 butterfly j of every slot");
+    __shared__ __align__(16) float2 lds[E::LDS_ELEMS];
+    __shared__ float2 twl[TW::kLdsEntries];
+    static_assert(R0 * NJ * 16 <= E::LDS_ELEMS * 8, "the factor exchange fits the idle image");
+    float4* xch = reinterpret_cast<float4*>(lds);  // (e.x, e.y, 1/|k|) of texel j + r NJ of row y1, r < 4
+    TW::load(twl, v.tw, threadIdx.x, T);
+    const float2* tws = twl;
+    __shared__ WaveBand band[kMaxCascades];
+    if ((int)threadIdx.x < v.C) band[threadIdx.x] = wave_band(v.casc + threadIdx.x * 5);
+    const int j = (int)threadIdx.x;
+    const bool j0 = (j == 0);
+    const int jm = (NJ - j) & (NJ - 1);
+    const int par = v.xpar;
+    const float sgn = par ? -1.0f : 1.0f;
+    // iteration r (texel pairs r, r + 4) folds z of row y1 at slot r and of row y2 at slot i2(r)
+    auto i2 = [&](int r) { return j0 ? ((R0 - r) & (R0 - 1)) : (R0 - 1 - r); };
+    float2 zt1[R0], zt2[R0];  // w_N^{b n'} at n' = j + r NJ (row y1) and jm + i2(r) NJ (row y2), by iteration r
+#pragma unroll
+    for (int r = 0; r < R0; ++r) {
+        zt1[r] = par ? v.tw[j + r * NJ] : make_float2(1.0f, 0.0f);
+        zt2[r] = par ? v.tw[jm + i2(r) * NJ] : make_float2(1.0f, 0.0f);
+    }
+    auto rows_of = [&](int it, int& u, int& y1, int& y2) {
+        u = it / IPU;
+        y1 = it - u * IPU;
+        y2 = (N - y1) & (N - 1);
+    };
+    float2 A[2 * R0], B[2 * R0];
+    auto load_pair = [&](int it) {
+        int u, y1, y2;
+        rows_of(it, u, y1, y2);
+        const float2* r1 = v.h0k + ((size_t)u * N + y1) * N;
+        const float2* r2 = v.h0k + ((size_t)u * N + y2) * N;
+#pragma unroll
+        for (int r = 0; r < 2 * R0; ++r) {
+            A[r] = r1[j + r * NJ];
+            B[r] = r2[(N - j - r * NJ) & (N - 1)];
+        }
+    };
+    int it = blockIdx.x;
+    if (it < items) load_pair(it);
+    __syncthreads();  // twiddles, band
+    for (; it < items; it += gridDim.x) {
+        int u, y1, y2;
+        rows_of(it, u, y1, y2);
+        const WaveBand wb = band[(u + v.c0) % v.C];
+        const bool self = (y1 == y2);
+        float4 own[R0];
+#pragma unroll
+        for (int r = 0; r < R0; ++r) {
+            own[r] = mirror_factors<N>(j + r * NJ, y1, wb, v.gravity, time);
+            xch[r * NJ + j] = own[r];
+        }
+        __syncthreads();
+        float2 in[7][R0];  // slots 0-2 row y1, 3-5 row y2, 6 srow (stage-0 input order)
+#pragma unroll
+        for (int r = 0; r < R0; ++r) {
+            float2 qa[2][4], qb[2][3];  // texel pairs r (lo) and r + 4 (hi): Q1..Q3 (+ row 0's Q4) at k, Q1..Q3 at -k
+#pragma unroll
+            for (int hi = 0; hi < 2; ++hi) {
+                const int rr = r + hi * R0;
+                float4 f;
+                if (hi == 0) {
+                    f = own[r];
+                } else {
+                    const int rp = j0 ? 2 * R0 - rr : 2 * R0 - 1 - rr;  // the in-row mirror's r' (< 4, or 4 on lane 0)
+                    f = (rp < R0) ? xch[(rp & (R0 - 1)) * NJ + jm] : mirror_factors<N>(j + rr * NJ, y1, wb, v.gravity, time);
+                }
+                const float4 wd = make_float4((float)(j + rr * NJ - N / 2) * wb.dk, f.z, (float)(y1 - N / 2) * wb.dk, 0.0f);
+                const float2 h = evolve_h(make_float4(A[rr].x, A[rr].y, B[rr].x, -B[rr].y), Phase{f.x, f.y});
+                QTex a, b;
+                qa[hi][3] = make_float2(0.0f, 0.0f);
+                if (y1 != 0 && !(rr == 0 && j0)) {
+                    q_fast(h, wd, a, b);
+                } else {  // Nyquist lines (see pass AQ)
+                    const float4 wm = make_float4((j0 && rr == 0) ? wd.x : -wd.x, wd.y, y1 ? -wd.z : wd.z, wd.w);
+                    const Planes4 o = planes_of(h, wd), om = planes_of(make_float2(h.x, -h.y), wm);
+                    q_planes(o, om, a, b);
+                    if (y1 == 0) qa[hi][3] = q4_full(o, om);
+                    if (rr == 0 && j0) {
+                        float2* side = q_side(v, u);
+                        side[y1] = q4_minus(o, om, wd.z);
+                        side[y2] = q4_minus(om, o, wm.z);
+                    }
+                }
+#pragma unroll
+                for (int p = 0; p < 3; ++p) {
+                    qa[hi][p] = a.q[p];
+                    qb[hi][p] = b.q[p];
+                }
+            }
+            // row y1: z[j + r NJ] = Q(x_r) + s Q(x_{r+4});  row y2 (slot i2(r)): Q(N - x_{r+4}) + s Q(N - x_r),
+            // except lane 0, r = 0 (texels 0 and N/2 map onto themselves): Q(N - x_0) + s Q(N - x_4)
+            const bool swap2 = j0 && r == 0;
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                if (p == 3 && y1 != 0) {
+                    in[6][r] = make_float2(0.0f, 0.0f);
+                    continue;
+                }
+                const float2 z1 = make_float2(qa[0][p].x + sgn * qa[1][p].x, qa[0][p].y + sgn * qa[1][p].y);
+                in[p == 3 ? 6 : p][r] = par ? cmul(z1, zt1[r]) : z1;
+                if (p < 3) {
+                    const float2 a2 = swap2 ? qb[0][p] : qb[1][p], b2 = swap2 ? qb[1][p] : qb[0][p];
+                    const float2 z2 = make_float2(a2.x + sgn * b2.x, a2.y + sgn * b2.y);
+                    in[3 + p][R0 - 1 - r] = par ? cmul(z2, zt2[r]) : z2;  // position i2(r) off lane 0
+                }
+            }
+        }
+        // lane 0: iteration r belongs at position (4 - r) & 3, not 3 - r: rotate positions by one
+        if (j0) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                const float2 t = in[3 + p][3];
+                in[3 + p][3] = in[3 + p][2];
+                in[3 + p][2] = in[3 + p][1];
+                in[3 + p][1] = in[3 + p][0];
+                in[3 + p][0] = t;
+            }
+        }
+        const int next = it + gridDim.x;
+        if (EARLY_PF && next < items) load_pair(next);  // the next pair's h0k in flight across the stages
+#pragma unroll
+        for (int s = 0; s < 7; ++s) Idft<R0>::run(in[s]);
+        __syncthreads();  // every lane has read the exchange off the image
+        const int live = (y1 == 0) ? 7 : 6;
+#pragma unroll
+        for (int s = 0; s < 7; ++s) {
+            if (s == 6 && y1 != 0) continue;
+            float2* dst = lds + E::lidx(s, ((s >= 3 && s < 6) ? jm : j) * R0);
+#pragma unroll
+            for (int q = 0; q < R0; ++q) dst[E::loff(q, 1)] = in[s][q];
+        }
+        __syncthreads();
+        auto emit = [&](int m, int q, float2 val) {
+            int b, jj;
+            E::template bj<E::RL>((int)threadIdx.x + m * T, b, jj);
+            const int mm = jj + q * NSL;  // compact column: x = 2 mm + parity
+            if (b == 6) {
+                if (y1 == 0) q_side(v, u)[N + mm] = val;  // srow
+                return;
+            }
+            if (b >= 3 && self) return;  // the self-mirror row's duplicate
+            const int p = b >= 3 ? b - 3 : b;
+            float2* rowp = v.tplane + (size_t)p * v.inter_stride + ((size_t)u * TILES * N + (b >= 3 ? y2 : y1)) * W;
+            float2* dst = rowp + (size_t)(jj / W) * N * W + (jj % W);
+            dst[(size_t)q * (NSL / W) * N * W] = val;
+        };
+        E::template stages_from<1>(lds, tws, emit, live);
+        __syncthreads();
+        if (!EARLY_PF && next < items) load_pair(next);
+    }
+}
+
 // Pass BQ: per (unit, W-column tile), four column transforms from three planes:
 //   step 0: R[Q2] -> (Dy, Dyx)          kept (LDS)
 //   step 1: R[Q1] -> (Dx, Dz)           DISP = (Dx, Dy, Dz, 1); Dyx moves to registers; before the
@@ -824,6 +1000,18 @@ hipError_t launch_pass_a_q(const DevView& v, float t, hipStream_t s) {
         if (v.n != 4096 || v.x0 != 0 || v.nx != v.n / 2) return hipErrorInvalidValue;
         constexpr int T = 4096 / 8;
         const int total = v.units * 4096;
+        static const int pair = env_int_q("OCEAN_A3P_PAIR", 0);  // 1: mirror-pair rows (pass A3PP; A/B)
+        if (pair && v.h0k) {
+            const int items = v.units * (4096 / 2 + 1);
+            if (pair == 2) {  // next pair's h0k loaded after the stages
+                const int g = grid_q(k_pass_a3pp<4096, false>, T, items);
+                launch((k_pass_a3pp<4096, false>), dim3(g), dim3(T), 0, s, v, t, items);
+                return hipGetLastError();
+            }
+            const int g = grid_q(k_pass_a3pp<4096>, T, items);
+            launch((k_pass_a3pp<4096>), dim3(g), dim3(T), 0, s, v, t, items);
+            return hipGetLastError();
+        }
         static const int share = env_int_q("OCEAN_A3P_SHARE", 1);  // 0: every texel evaluates its own factors (A/B)
         if (!share) {
             const int g = grid_q(k_pass_a3p<4096, A3P_EARLY_PF, false>, T, total);

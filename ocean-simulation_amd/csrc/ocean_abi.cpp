@@ -459,7 +459,8 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
     bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
     ok = ok && alloc((void**)&c->noise, tex * c->T * 8);
     ok = ok && alloc((void**)&c->h0, tex * U * 16);
-    if (ocean::pass_a4_supported(n, c->P)) ok = ok && alloc((void**)&c->h0k, tex * U * 8);
+    // h0k: the mirror-pair row passes (N = 512 / 1024; at 4096 the column-parity pass A3PP)
+    if (ocean::pass_a4_supported(n, c->P) || (n == 4096 && c->P == 4)) ok = ok && alloc((void**)&c->h0k, tex * U * 8);
     ok = ok && alloc((void**)&c->waves, tex * U * 16);
     ok = ok && alloc((void**)&c->plane[0], tex * U * 8 * c->P);  // planes contiguous (one descriptor in pass A)
     if (ok)
