@@ -8,8 +8,8 @@ A "step" is one ocean frame: ocean_step(t) = evolve -> 2D IFFT of every plane
 minus GenerateMips), inputs resident in HBM.  Multi-GPU: one process per GPU
 (torchrun).  cfg2/cfg3 scale weakly (every rank runs its own ocean); cfg4 and
 cfg5 split one job (ocean_hip.shard.plan_shard: tile blocks for cfg4; cascades,
-then column bands for cfg5 -- at 8 GPUs each rank owns one 4096^2 cascade's half
-columns).  No data-path collective exists; gloo carries only the
+then even / odd columns for cfg5 -- at 8 GPUs each rank owns one 4096^2 cascade's
+even or odd columns, ocean_set_column_parity).  No data-path collective exists; gloo carries only the
 start/stop barrier and the max-over-ranks of the elapsed time.  `value` =
 ocean-frames of the configured job (4 x 1024^2 cascades for cfg3) completed per
 second over all ranks.  Rank 0 prints ONE JSON line.
@@ -52,7 +52,7 @@ CONFIGS = {
     "cfg4": dict(n=512, cascades=4, tiles=256, disp_only=False, per_rank=False,
                  desc="256 tiles x 4 x 512^2 cascades, sharded over ranks"),
     "cfg5": dict(n=4096, cascades=4, tiles=1, disp_only=False, per_rank=False,
-                 desc="4 x 4096^2 cascades, split over ranks (cascades, then column bands)"),
+                 desc="4 x 4096^2 cascades, split over ranks (cascades, then even / odd columns)"),
 }
 
 
@@ -356,7 +356,7 @@ def main():
     else:
         # strong scaling: the job's fixed oceans split over the ranks -- contiguous tile
         # blocks (cfg4), or one ocean's cascades and then column bands (cfg5 on 8 GPUs:
-        # one cascade, half the columns per rank); no data exchange either way
+        # one cascade's even or odd columns per rank); no data exchange either way
         sh = plan_shard(cfg["tiles"], cfg["cascades"], n, world, rank, interleave=not args.no_interleave)
         first, tiles, casc0, C, x0, nx = sh.tile0, sh.tiles, sh.casc0, sh.cascades, sh.x0, sh.nx
         parity = sh.parity
