@@ -257,6 +257,7 @@ def ifft_beyond_cache(reps=50):
         ctx.evolve(0.5)  # planes with the frame's data (the transform's time does not depend on it)
         r = ifft_measure(ctx, reps, "ifft_bc_kernel_stats.csv", "ifft_bc")
         r["workload"] = "4 tiles x 4 cascades x 1024^2, 4 planes: 512 MiB of planes (2x the Infinity Cache)"
+        r["data"] = "planes of ocean_evolve(0.5) (frame data)"
         return r
     finally:
         ctx.close()
@@ -456,9 +457,13 @@ def main():
 
     ifft_stage = None
     if not args.no_ifft_stage and not cfg["disp_only"]:
-        # operator-level stage (IFFT.InverseFastFourierTransform x 4 planes), unfused kernels
+        # operator-level stage (IFFT.InverseFastFourierTransform x 4 planes), unfused kernels, on the
+        # frame's own planes (ocean_evolve): the fused frame never writes them, and zero-filled planes
+        # run at a higher clock (MI355X_MICROARCH.md) -- rounds 1-2 timed the operator on zeros
+        ctx.evolve(args.warmup / 60.0)
         ifft_stage = ifft_measure(ctx, max(20, args.steps // 5), "ifft_kernel_stats.csv",
                                   "cfg3" if args.config == "cfg3" else None)
+        ifft_stage["data"] = "planes of ocean_evolve(t) (frame data)"
         if rank == 0 and world == 1 and args.config == "cfg3" and not args.no_beyond_cache:
             ifft_stage["beyond_cache"] = ifft_beyond_cache()
 

@@ -18,6 +18,13 @@ reps = int(sys.argv[4]) if len(sys.argv) > 4 else 50
 mask = int(sys.argv[5]) if len(sys.argv) > 5 else 0b1111
 planes = bin(mask).count("1")
 ctx = oh.OceanContext(n, C, T, oh.F_UNFUSED)
+# the frame's own data in the planes (zero-filled planes run at a higher clock, MI355X_MICROARCH.md)
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import bench  # noqa: E402
+ctx.set_params(bench.SCENE_PARAMS, (bench.SCENE_CASCADES * 2)[:C])
+ctx.generate_noise_device(20251121)
+ctx.init_spectrum()
+ctx.evolve(0.5)
 for _ in range(5):
     ctx.ifft2d(mask)
 ctx.synchronize()
