@@ -198,26 +198,37 @@ def ifft_measure(ctx, reps, csv_name, pmc_config):
     """The operator IFFT (ocean_ifft2d over the 4 planes, IFFT.InverseFastFourierTransform x 4) of a
     context: wall time (no events) and kernel time (HIP events attached to every launch) per call,
     algorithmic bytes 32 B per texel per plane (two passes x read + write), the symbols of the row
-    and column kernels that ran, and the committed rocprofv3 / PMC records of exactly those symbols."""
+    and column kernels that ran, and the committed rocprofv3 / PMC records of exactly those symbols.
+    Every call transforms freshly evolved planes (ocean_evolve before it): the unnormalised inverse
+    transform grows the data by ~N per call, to inf / NaN within a dozen calls, and constant or zero
+    data runs at a higher clock (MI355X_MICROARCH.md).  Wall = (evolve + operator) - (evolve alone)."""
     n, units = ctx.n, ctx.C * ctx.T
-    for _ in range(5):  # first launches load the row/column code objects: keep them out of the timing
+    for k in range(5):  # first launches load the row/column code objects: keep them out of the timing
+        ctx.evolve(0.1 * k)
         ctx.ifft2d(0b1111)
     ctx.synchronize()
-    s0 = time.perf_counter()  # wall region: no events
-    for _ in range(reps):
+    s0 = time.perf_counter()  # wall regions: no events
+    for k in range(reps):
+        ctx.evolve(0.5 + k / 60.0)
         ctx.ifft2d(0b1111)
     ctx.synchronize()
     s1 = time.perf_counter()
-    ctx.set_kernel_timing(True)  # kernel region: events around every launch
+    for k in range(reps):
+        ctx.evolve(0.5 + k / 60.0)
+    ctx.synchronize()
+    s2 = time.perf_counter()
+    ctx.set_kernel_timing(True)  # kernel region: events around every launch (evolve is kind 2)
     ctx.kernel_stats(0), ctx.kernel_stats(1), ctx.kernel_stats(2)
-    for _ in range(reps):
+    for k in range(reps):
+        ctx.evolve(0.5 + k / 60.0)
         ctx.ifft2d(0b1111)
     r_ms, r_n = ctx.kernel_stats(0)
     c_ms, c_n = ctx.kernel_stats(1)
+    ctx.kernel_stats(2)
     ctx.set_kernel_timing(False)
     syms = {"rows": ctx.kernel_name(0), "cols": ctx.kernel_name(1)}
     fft_bytes = 32 * n * n * 4 * units
-    stage_us = 1e6 * (s1 - s0) / reps
+    stage_us = 1e6 * ((s1 - s0) - (s2 - s1)) / reps
     kern_us = 1e3 * (r_ms + c_ms) / reps
     rp = {k: rocprof_kernel_us(csv_name, v) for k, v in syms.items()}
     rocprof = None
@@ -254,10 +265,9 @@ def ifft_beyond_cache(reps=50):
         ctx.set_params(SCENE_PARAMS, SCENE_CASCADES)
         ctx.generate_noise_device(20251121)
         ctx.init_spectrum()
-        ctx.evolve(0.5)  # planes with the frame's data (the transform's time does not depend on it)
         r = ifft_measure(ctx, reps, "ifft_bc_kernel_stats.csv", "ifft_bc")
         r["workload"] = "4 tiles x 4 cascades x 1024^2, 4 planes: 512 MiB of planes (2x the Infinity Cache)"
-        r["data"] = "planes of ocean_evolve(0.5) (frame data)"
+        r["data"] = "freshly evolved planes before every call (frame data)"
         return r
     finally:
         ctx.close()
@@ -458,12 +468,11 @@ def main():
     ifft_stage = None
     if not args.no_ifft_stage and not cfg["disp_only"]:
         # operator-level stage (IFFT.InverseFastFourierTransform x 4 planes), unfused kernels, on the
-        # frame's own planes (ocean_evolve): the fused frame never writes them, and zero-filled planes
-        # run at a higher clock (MI355X_MICROARCH.md) -- rounds 1-2 timed the operator on zeros
-        ctx.evolve(args.warmup / 60.0)
+        # frame's own planes (ocean_evolve before every call): the fused frame never writes them, and
+        # zero-filled planes run at a higher clock (MI355X_MICROARCH.md) -- rounds 1-2 timed zeros
         ifft_stage = ifft_measure(ctx, max(20, args.steps // 5), "ifft_kernel_stats.csv",
                                   "cfg3" if args.config == "cfg3" else None)
-        ifft_stage["data"] = "planes of ocean_evolve(t) (frame data)"
+        ifft_stage["data"] = "freshly evolved planes before every call (frame data)"
         if rank == 0 and world == 1 and args.config == "cfg3" and not args.no_beyond_cache:
             ifft_stage["beyond_cache"] = ifft_beyond_cache()
 
