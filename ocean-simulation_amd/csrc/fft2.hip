@@ -75,10 +75,11 @@ __global__ __launch_bounds__(B * N / kElems) void k_rows2(const float2* plane, f
 // 128-byte line still moves through one L2.
 constexpr int cols2_w(int N) { return N == 1024 ? 16 : col_tile(N); }
 
-// XP (W = 8 at N = 1024): the two 8-column halves of a 16-column tile go to items i and i + 8,
-// which blocks b and b + 8 -- one XCD under round-robin placement (speed only, never correctness)
-// -- take at the same time, so each 128-byte line is fetched and written back through one L2.
-template <int N, int W_ = cols2_w(N), bool XP = false>
+// G > 1 (XCD grouping): the G W-column pieces of a (G W)-column tile go to items i, i + 8, ...,
+// i + 8 (G - 1), which blocks b, b + 8, ... -- one XCD under round-robin placement (speed only, never
+// correctness) -- take at the same time, so each 128-byte line is fetched and written back through one
+// L2.  G = 2, W = 8 at N = 1024; G = 4, W = 4 at N = 2048 / 4096 (OCEAN_COLS2_XQ).
+template <int N, int W_ = cols2_w(N), int G = 1>
 __global__ __launch_bounds__(W_ * N / kElems) void k_cols2(float2* __restrict__ plane, int items,
                                                           const float2* __restrict__ tw) {
     using CT = ColTile<N, W_>;
@@ -94,7 +95,7 @@ __global__ __launch_bounds__(W_ * N / kElems) void k_cols2(float2* __restrict__ 
     float2 cur[kElems], nxt[kElems];
     // item -> tile index (unit * tiles + tile)
     auto tile_of = [&](int item) {
-        if constexpr (XP) return (item & ~15) + 2 * (item & 7) + ((item >> 3) & 1);
+        if constexpr (G > 1) return (item & ~(8 * G - 1)) + G * (item & 7) + ((item >> 3) & (G - 1));
         else return item;
     };
     auto win = [&](int item) {
@@ -322,13 +323,13 @@ struct Rows2 {
 };
 template <int N>
 struct Cols2 {
-    template <int W, bool XP>
+    template <int W, int G>
     static hipError_t go_w(const DevView* v, float2* base, int ups, hipStream_t s) {
         constexpr int T = W * N / kElems;
         const int items = ups * (N / W);
-        int g = persistent_grid(k_cols2<N, W, XP>, T, items);
-        if (XP) g -= g % 16;  // halves of a tile on blocks b, b + 8 at every step of the item loop
-        launch((k_cols2<N, W, XP>), dim3(g), dim3(T), 0, s, base, items, v->tw);
+        int g = persistent_grid(k_cols2<N, W, G>, T, items);
+        if (G > 1) g -= g % (8 * G);  // pieces of a tile on blocks b, b + 8, ... at every step of the item loop
+        launch((k_cols2<N, W, G>), dim3(g), dim3(T), 0, s, base, items, v->tw);
         return hipGetLastError();
     }
     static hipError_t go(const DevView* v, float2* base, int ups, hipStream_t s) {
@@ -336,9 +337,20 @@ struct Cols2 {
             // default: 8-column halves paired on one XCD (45.6 against 49.7 us for 4 x 1024^2 x 4 planes);
             // OCEAN_COLS2_XP=0 selects the 16-column tiles (A/B)
             static const int xp = std::getenv("OCEAN_COLS2_XP") ? std::atoi(std::getenv("OCEAN_COLS2_XP")) : 1;
-            if (xp) return go_w<8, true>(v, base, ups, s);
+            if (xp) return go_w<8, 2>(v, base, ups, s);
         }
-        return go_w<cols2_w(N), false>(v, base, ups, s);
+        if constexpr (N >= 2048) {
+            // default: column pieces of 16-column tiles grouped on one XCD -- 8-column halves at 2048,
+            // 4-column quarters at 4096 (whole columns in LDS: 128 KiB) -- 0.65 / 0.57 of peak against
+            // 0.25 / 0.26 ungrouped (4 columns, 32-byte row pieces).  OCEAN_COLS2_XQ: 0 ungrouped, 1 4 x 4,
+            // 2 2 x 8, 3 8 x 2 (2048) -- A/B
+            static const int xq = std::getenv("OCEAN_COLS2_XQ") ? std::atoi(std::getenv("OCEAN_COLS2_XQ")) : -1;
+            if (xq == 1 || (xq < 0 && N == 4096)) return go_w<4, 4>(v, base, ups, s);
+            if (xq == 2) return go_w<2, 8>(v, base, ups, s);
+            if constexpr (N == 2048)
+                if (xq == 3 || xq < 0) return go_w<8, 2>(v, base, ups, s);
+        }
+        return go_w<cols2_w(N), 1>(v, base, ups, s);
     }
 };
 // Four-step operator for N = 2048 / 4096 over `ups` consecutive unit-planes at `planes` (one

@@ -151,7 +151,7 @@ struct ocean_ctx {
     int c4_bands = 0;        // OCEAN_C4_BANDS: N >= 2048 column passes per (unit, band); 0 = auto
     int chunk_min = 1 << 30; // OCEAN_CHUNK_MIN: units per chunk when one unit exceeds OCEAN_CHUNK_MIB
     int chunk_reuse = 1;     // OCEAN_CHUNK_REUSE=0: one intermediate region per unit (A/B)
-    int op_four_step = 1;    // OCEAN_OP_FOUR_STEP=0: ocean_ifft2d at N >= 2048 through k_rows2 / k_cols2 (A/B)
+    int op_four_step = 0;    // OCEAN_OP_FOUR_STEP=1: ocean_ifft2d at N >= 2048 through four-step columns (A/B)
     long op_chunk_mib = 0;   // OCEAN_OP_CHUNK_MIB: MiB of unit-planes per chunk of the operator IFFT (0: auto)
     size_t inter_units = 0;  // units the intermediate holds (a chunk's, or all with chunk_reuse = 0)
     int band_x0 = 0, band_nx = 0;  // column band of the fused passes (ocean_set_column_band); nx = n: whole
@@ -648,6 +648,8 @@ int ocean_ifft2d(ocean_ctx* ctx, int plane_mask) {
         int np = 1;  // run of consecutive planes: one launch per direction (planes are one allocation)
         while (p + np < 4 && (plane_mask & (1 << (p + np)))) ++np;
         if (ctx->n >= 2048 && ctx->op_four_step) {
+            // A/B (OCEAN_OP_FOUR_STEP=1; round 3's first N >= 2048 operator, 0.47 of peak at 4 x 4096^2
+            // against 0.63 for the default below):
             // four-step columns (fft2.hip): per chunk of unit-planes, rows -> scratch (the fused
             // intermediate's room), C1 on the scratch, C2 scratch -> planes; a chunk of at most
             // OCEAN_OP_CHUNK_MIB stays in the Infinity Cache between the three launches
@@ -673,10 +675,12 @@ int ocean_ifft2d(ocean_ctx* ctx, int plane_mask) {
             p += np;
             continue;
         }
-        // N <= 1024: in-place row and column launches per chunk of at most OCEAN_OP_CHUNK_MIB of
-        // unit-planes, so the column launch re-reads the rows' output from the Infinity Cache when the
-        // plane set is larger than it.  Auto: 256 MiB (4 x 4 x 1024^2 x 4 planes, 512 MiB: 64 / 128 /
-        // 192 / 256 MiB / unchunked 0.66 / 0.70 / 0.71 / 0.735 / 0.54 of peak; cfg3's 128 MiB: one chunk)
+        // In-place row and column launches per chunk of at most OCEAN_OP_CHUNK_MIB of unit-planes, so
+        // the column launch re-reads the rows' output from the Infinity Cache when the plane set is
+        // larger than it.  Auto: 256 MiB (4 x 4 x 1024^2 x 4 planes, 512 MiB, fresh data: 128 / 192 /
+        // 256 / 320 / 384 MiB / unchunked 0.69 / 0.69 / 0.736 / 0.63 / 0.60 / 0.57 of peak; cfg3's 128
+        // MiB: one chunk; 4096^2 x 4 planes: 128 / 256 / 512 MiB 0.59 / 0.63 / 0.44).  At N >= 2048 the
+        // column launch takes XCD-grouped pieces of 16-column tiles (fft2.hip Cols2).
         const int ups = np * (int)ctx->units();
         const long mib = ctx->op_chunk_mib > 0 ? ctx->op_chunk_mib : 256;
         const int k = (int)std::max<size_t>(1, ((size_t)mib << 20) / (up_elems * 8));

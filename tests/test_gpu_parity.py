@@ -102,11 +102,15 @@ def test_ifft2d_operator_vs_oracle(n):
     ctx.close()
 
 
-@pytest.mark.parametrize("n,C,mask", [(2048, 1, 0b0001), (4096, 4, 0b1111)])
-def test_ifft2d_operator_large_vs_numpy(n, C, mask):
-    """The operator at N = 2048 / 4096 (four-step column passes through the scratch, fft2.hip) on
-    every requested plane of every cascade, against numpy's float64 ifft2 (ref64); 4 x 4096^2 x 4
-    planes is cfg5's whole plane set (2 GiB), one unit-plane per chunk."""
+@pytest.mark.parametrize("n,C,mask,four_step", [(2048, 1, 0b0001, False), (4096, 4, 0b1111, False),
+                                                 (2048, 1, 0b0001, True), (4096, 4, 0b1111, True)])
+def test_ifft2d_operator_large_vs_numpy(n, C, mask, four_step, monkeypatch):
+    """The operator at N = 2048 / 4096 on every requested plane of every cascade, against numpy's
+    float64 ifft2 (ref64); 4 x 4096^2 x 4 planes is cfg5's whole plane set (2 GiB).  Default: in-place
+    rows, then whole-column tiles grouped on one XCD, two unit-planes per chunk at 4096 (fft2.hip
+    Cols2); four_step: the A/B four-step column passes through the scratch (OCEAN_OP_FOUR_STEP=1)."""
+    if four_step:
+        monkeypatch.setenv("OCEAN_OP_FOUR_STEP", "1")
     ctx = oh.OceanContext(n, C, 1)
     planes = [p for p in range(4) if mask >> p & 1]
 
@@ -126,13 +130,15 @@ def test_ifft2d_operator_large_vs_numpy(n, C, mask):
     ctx.close()
 
 
-@pytest.mark.parametrize("chunk_mib", [None, 64])
-def test_ifft2d_operator_2048_vs_oracle(chunk_mib, monkeypatch):
+@pytest.mark.parametrize("chunk_mib,four_step", [(None, False), (64, False), (None, True), (64, True)])
+def test_ifft2d_operator_2048_vs_oracle(chunk_mib, four_step, monkeypatch):
     """N = 2048 operator against the reference's radix-2 schedule (oracle) on three planes of two
     cascades (6 unit-planes of 32 MiB): one chunk by default, or 3 chunks of 2 unit-planes at
-    OCEAN_OP_CHUNK_MIB=64; plane 3 untouched."""
+    OCEAN_OP_CHUNK_MIB=64; plane 3 untouched; default and four-step (OCEAN_OP_FOUR_STEP=1) columns."""
     if chunk_mib:
         monkeypatch.setenv("OCEAN_OP_CHUNK_MIB", str(chunk_mib))
+    if four_step:
+        monkeypatch.setenv("OCEAN_OP_FOUR_STEP", "1")
     n, C = 2048, 2
     ctx = oh.OceanContext(n, C, 1)
     rng = np.random.default_rng(7)
