@@ -897,7 +897,9 @@ int step_fused(ocean_ctx* ctx, float time) {
             continue;
         }
         if (int r = timed(ctx, 0, [&] {
-                if (ctx->a4 && ctx->h0k_valid) return ocean::launch_pass_a_v4(c, time, ctx->stream);
+                // h0k also exists at 4096 (pass A3PP), where the mirror-pair pass A4 does not
+                if (ctx->a4 && ctx->h0k_valid && ocean::pass_a4_supported(ctx->n, ctx->P))
+                    return ocean::launch_pass_a_v4(c, time, ctx->stream);
                 return ocean::launch_pass_a_v3(c, time, ctx->stream);
             }, "pass_a"))
             return r;
