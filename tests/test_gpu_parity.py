@@ -234,12 +234,14 @@ def oracle_threads():
 
 @pytest.mark.parametrize("n,ncasc,flags", [(256, 1, 0), (512, 1, oh.F_DISPLACEMENT_ONLY), (512, 3, 0),
                                            (1024, 4, 0), (1024, 4, oh.F_UNFUSED), (2048, 1, 0),
-                                           (4096, 1, 0), (4096, 1, oh.F_DISPLACEMENT_ONLY), (4096, 4, 0)])
+                                           (2048, 1, oh.F_UNFUSED), (4096, 1, 0), (4096, 1, oh.F_UNFUSED),
+                                           (4096, 1, oh.F_DISPLACEMENT_ONLY), (4096, 4, 0)])
 def test_frames_vs_oracle(n, ncasc, flags):
     """BASELINE configs: cfg1-shaped 256^2 x1, cfg2 512^2 displacement only, the scene (512^2 x3),
     cfg3 4 x 1024^2 full outputs, one cfg5 cascade at 4096^2 and cfg5 whole (4 x 4096^2: a 2 GiB
     plane array, 2^31 bytes) through the four-step column passes, against the radix-2 oracle at
-    full size; 3 frames (2 for cfg5 whole) so the foam state is exercised."""
+    full size; 3 frames (2 for cfg5 whole) so the foam state is exercised.  F_UNFUSED at 2048 / 4096:
+    the reference-shaped frame through the operator IFFT's XCD-grouped whole-column tiles."""
     cas = O.SCENE_CASCADES[:ncasc]
     ctx, (noise,) = make_ctx(n, cas, flags=flags)
     nplanes = 2 if flags & oh.F_DISPLACEMENT_ONLY else 4
