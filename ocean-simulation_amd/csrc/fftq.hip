@@ -612,12 +612,13 @@ __global__ __launch_bounds__(N / 8) A3P_WPEU void k_pass_a3p(DevView v, float ti
 // y2 at butterfly jm = (N/8 - j) % (N/8).  Eight sequence slots, two radix-16 butterflies per lane
 // per LDS stage: 0-2 Q1..Q3 of row y1, 3-5 of row y2, 6 row 0's srow, 7 idle.  The self-mirror rows
 // 0 and N/2 run the same code; their y2 slots duplicate y1 and are not stored.
-template <int N, bool EARLY_PF = true>
-__global__ __launch_bounds__(N / 8) void k_pass_a3pp(DevView v, float time, int items) {
+// FIRST = 2 (OCEAN_A3P_PAIR=3/4): N/4 lanes, texels j + r N/4 (r < 4), a radix-2 first stage and one
+// radix-16 butterfly per lane per LDS stage -- 16 waves per workgroup instead of 8.
+template <int N, bool EARLY_PF = true, int FIRST = 4>
+__global__ __launch_bounds__(N / (2 * FIRST)) void k_pass_a3pp(DevView v, float time, int items) {
     constexpr int H = N / 2;  // transform length
-    constexpr int FIRST = 4;
     using TW = StageTwCompactSub<H, N, FIRST>;
-    using E = Engine<H, 8, false, true, FIRST, TW, 32>;
+    using E = Engine<H, 8, false, true, FIRST, TW, 8 * FIRST>;
     constexpr int T = E::THREADS;
     constexpr int R0 = E::R0;
     constexpr int NJ = H / R0;  // lanes = texel stride
@@ -625,11 +626,11 @@ __global__ __launch_bounds__(N / 8) void k_pass_a3pp(DevView v, float time, int 
     constexpr int TILES = N / W;
     constexpr int NSL = H / E::RL;
     constexpr int IPU = N / 2 + 1;  // items per unit
-    static_assert(T == NJ && R0 == 4 && T == N / 8, "lane j <-> stage-0 butterfly j of every slot");
+    static_assert(T == NJ && R0 == FIRST && T == N / (2 * FIRST), "lane j <-> stage-0 butterfly j of every slot");
     __shared__ __align__(16) float2 lds[E::LDS_ELEMS];
     __shared__ float2 twl[TW::kLdsEntries];
     static_assert(R0 * NJ * 16 <= E::LDS_ELEMS * 8, "the factor exchange fits the idle image");
-    float4* xch = reinterpret_cast<float4*>(lds);  // (e.x, e.y, 1/|k|) of texel j + r NJ of row y1, r < 4
+    float4* xch = reinterpret_cast<float4*>(lds);  // (e.x, e.y, 1/|k|) of texel j + r NJ of row y1, r < R0
     TW::load(twl, v.tw, threadIdx.x, T);
     const float2* tws = twl;
     __shared__ WaveBand band[kMaxCascades];
@@ -641,12 +642,23 @@ __global__ __launch_bounds__(N / 8) void k_pass_a3pp(DevView v, float time, int 
     const float sgn = par ? -1.0f : 1.0f;
     // iteration r (texel pairs r, r + 4) folds z of row y1 at slot r and of row y2 at slot i2(r)
     auto i2 = [&](int r) { return j0 ? ((R0 - r) & (R0 - 1)) : (R0 - 1 - r); };
-    float2 zt1[R0], zt2[R0];  // w_N^{b n'} at n' = j + r NJ (row y1) and jm + i2(r) NJ (row y2), by iteration r
+    // w_N^{b n'} at n' = j + r NJ (row y1) and jm + i2(r) NJ (row y2), by iteration r.  FIRST = 2: NJ = N/4,
+    // w_N^{n + N/4} = i w_N^n, so two values and a quarter turn (8 VGPRs fewer at 128)
+    constexpr int NZ = FIRST == 2 ? 1 : R0;
+    float2 zt1[NZ], zt2[NZ];
 #pragma unroll
-    for (int r = 0; r < R0; ++r) {
+    for (int r = 0; r < NZ; ++r) {  // FIRST = 2: zt1[0] = w^j, zt2[0] = w^jm
         zt1[r] = par ? v.tw[j + r * NJ] : make_float2(1.0f, 0.0f);
-        zt2[r] = par ? v.tw[jm + i2(r) * NJ] : make_float2(1.0f, 0.0f);
+        zt2[r] = par ? v.tw[jm + (FIRST == 2 ? 0 : i2(r)) * NJ] : make_float2(1.0f, 0.0f);
     }
+    auto z1_at = [&](int r) {
+        if constexpr (FIRST == 2) return (r && par) ? cmul_i(zt1[0]) : zt1[0];
+        else return zt1[r];
+    };
+    auto z2_at = [&](int r) {  // i2(r) = 1 - r off lane 0, r on lane 0
+        if constexpr (FIRST == 2) return (i2(r) && par) ? cmul_i(zt2[0]) : zt2[0];
+        else return zt2[r];
+    };
     auto rows_of = [&](int it, int& u, int& y1, int& y2) {
         u = it / IPU;
         y1 = it - u * IPU;
@@ -682,7 +694,7 @@ __global__ __launch_bounds__(N / 8) void k_pass_a3pp(DevView v, float time, int 
         float2 in[7][R0];  // slots 0-2 row y1, 3-5 row y2, 6 srow (stage-0 input order)
 #pragma unroll
         for (int r = 0; r < R0; ++r) {
-            float2 qa[2][4], qb[2][3];  // texel pairs r (lo) and r + 4 (hi): Q1..Q3 (+ row 0's Q4) at k, Q1..Q3 at -k
+            float2 qa[2][4], qb[2][3];  // texel pairs r (lo) and r + R0 (hi): Q1..Q3 (+ row 0's Q4) at k, Q1..Q3 at -k
 #pragma unroll
             for (int hi = 0; hi < 2; ++hi) {
                 const int rr = r + hi * R0;
@@ -690,7 +702,7 @@ __global__ __launch_bounds__(N / 8) void k_pass_a3pp(DevView v, float time, int 
                 if (hi == 0) {
                     f = own[r];
                 } else {
-                    const int rp = j0 ? 2 * R0 - rr : 2 * R0 - 1 - rr;  // the in-row mirror's r' (< 4, or 4 on lane 0)
+                    const int rp = j0 ? 2 * R0 - rr : 2 * R0 - 1 - rr;  // the in-row mirror's r' (< R0, or R0 on lane 0)
                     f = (rp < R0) ? xch[(rp & (R0 - 1)) * NJ + jm] : mirror_factors<N>(j + rr * NJ, y1, wb, v.gravity, time);
                 }
                 const float4 wd = make_float4((float)(j + rr * NJ - N / 2) * wb.dk, f.z, (float)(y1 - N / 2) * wb.dk, 0.0f);
@@ -726,22 +738,21 @@ __global__ __launch_bounds__(N / 8) void k_pass_a3pp(DevView v, float time, int 
                     continue;
                 }
                 const float2 z1 = make_float2(qa[0][p].x + sgn * qa[1][p].x, qa[0][p].y + sgn * qa[1][p].y);
-                in[p == 3 ? 6 : p][r] = par ? cmul(z1, zt1[r]) : z1;
+                in[p == 3 ? 6 : p][r] = par ? cmul(z1, z1_at(r)) : z1;
                 if (p < 3) {
                     const float2 a2 = swap2 ? qb[0][p] : qb[1][p], b2 = swap2 ? qb[1][p] : qb[0][p];
                     const float2 z2 = make_float2(a2.x + sgn * b2.x, a2.y + sgn * b2.y);
-                    in[3 + p][R0 - 1 - r] = par ? cmul(z2, zt2[r]) : z2;  // position i2(r) off lane 0
+                    in[3 + p][R0 - 1 - r] = par ? cmul(z2, z2_at(r)) : z2;  // position i2(r) off lane 0
                 }
             }
         }
-        // lane 0: iteration r belongs at position (4 - r) & 3, not 3 - r: rotate positions by one
+        // lane 0: iteration r belongs at position (R0 - r) & (R0 - 1), not R0 - 1 - r: rotate positions by one
         if (j0) {
 #pragma unroll
             for (int p = 0; p < 3; ++p) {
-                const float2 t = in[3 + p][3];
-                in[3 + p][3] = in[3 + p][2];
-                in[3 + p][2] = in[3 + p][1];
-                in[3 + p][1] = in[3 + p][0];
+                const float2 t = in[3 + p][R0 - 1];
+#pragma unroll
+                for (int q = R0 - 1; q > 0; --q) in[3 + p][q] = in[3 + p][q - 1];
                 in[3 + p][0] = t;
             }
         }
@@ -994,15 +1005,35 @@ bool pass_q_supported(int n, int planes) {
     return planes == 4 && (n == 512 || n == 1024 || n == 4096 || (n == 2048 && q2048));
 }
 
+// Row pass of a column-parity shard (OCEAN_A3P_PAIR): 4 (default) pass A3PP on 1024 lanes with the
+// next pair's h0k loaded after the stages; 3 the same with it in flight; 1 / 2 pass A3PP on 512 lanes
+// (early / late); 0 pass A3P (one row per item, full h0).  Pass A3PP needs a valid h0k (the caller
+// passes a null h0k after an H0 upload, and pass A3P runs).
+int pass_a3p_pair_mode() {
+    static const int pair = env_int_q("OCEAN_A3P_PAIR", 4);
+    return pair;
+}
+
 hipError_t launch_pass_a_q(const DevView& v, float t, hipStream_t s) {
     if (!pass_q_supported(v.n, v.planes) || !v.qside) return hipErrorInvalidValue;
     if (v.xstr == 2) {  // column parity (even / odd columns of every row)
         if (v.n != 4096 || v.x0 != 0 || v.nx != v.n / 2) return hipErrorInvalidValue;
         constexpr int T = 4096 / 8;
         const int total = v.units * 4096;
-        static const int pair = env_int_q("OCEAN_A3P_PAIR", 0);  // 1: mirror-pair rows (pass A3PP; A/B)
+        const int pair = pass_a3p_pair_mode();
         if (pair && v.h0k) {
             const int items = v.units * (4096 / 2 + 1);
+            if (pair == 3 || pair == 4) {  // 1024 lanes, radix-2 first stage (early / late next-pair h0k)
+                constexpr int T2 = 4096 / 4;
+                if (pair == 4) {
+                    const int g = grid_q(k_pass_a3pp<4096, false, 2>, T2, items);
+                    launch((k_pass_a3pp<4096, false, 2>), dim3(g), dim3(T2), 0, s, v, t, items);
+                } else {
+                    const int g = grid_q(k_pass_a3pp<4096, true, 2>, T2, items);
+                    launch((k_pass_a3pp<4096, true, 2>), dim3(g), dim3(T2), 0, s, v, t, items);
+                }
+                return hipGetLastError();
+            }
             if (pair == 2) {  // next pair's h0k loaded after the stages
                 const int g = grid_q(k_pass_a3pp<4096, false>, T, items);
                 launch((k_pass_a3pp<4096, false>), dim3(g), dim3(T), 0, s, v, t, items);

@@ -866,7 +866,8 @@ bool use_q(const ocean_ctx* ctx) {
 int step_fused(ocean_ctx* ctx, float time) {
     // pass A: mirror-pair rows (N = 512, 1024 with 4 planes and h0k valid) or per-texel
     // rows; pass B: column tiles (N <= 1024) or the four-step column passes (N >= 2048)
-    const ocean::DevView v = ctx->view();
+    ocean::DevView v = ctx->view();
+    if (!ctx->h0k_valid) v.h0k = nullptr;  // stale after an H0 upload: no row pass may read it
     const bool q = use_q(ctx);
     if (ctx->col_par >= 0 && !q)
         return fail(OCEAN_E_STATE, "a column parity needs the three-plane frame (h0 from ocean_init_spectrum)");
@@ -1235,7 +1236,9 @@ int ocean_step_bytes(ocean_ctx* ctx, uint64_t* pass_a, uint64_t* pass_b) {
             // three-plane frame (the side arrays, 16 B per row, not counted): pass A h0k (h0 at
             // N >= 2048) -> Q1..Q3; pass B Q1..Q3 + foam state -> outputs, or at N >= 2048 the
             // four-step passes: C1 reads Q1..Q3 and writes them with R[Q4], C2 reads four planes
-            *pass_a = tex * (ctx->n >= 2048 ? 16 : 8) + bt * 24;
+            // the column-parity row pass on mirror-pair rows (pass A3PP) reads h0k, 8 B per texel
+            const bool h0k_pairs = ctx->col_par >= 0 && ctx->h0k && ctx->h0k_valid && ocean::pass_a3p_pair_mode();
+            *pass_a = tex * ((ctx->n >= 2048 && !h0k_pairs) ? 16 : 8) + bt * 24;
             *pass_b = ctx->n >= 2048 ? bt * (24 + 32 + 32 + 8 + outs) : bt * (24 + 8 + outs);
             return OCEAN_OK;
         }

@@ -136,6 +136,7 @@ hipError_t launch_pass_a_v4(const DevView& v, float t, hipStream_t s);
 // (mirror-pair rows, N = 512 / 1024) or A3Q (one row per item, N = 2048 / 4096), then pass BQ
 // (column tiles, four transforms, N <= 1024) or the four-step column passes with Q planes.
 bool pass_q_supported(int n, int planes);
+int pass_a3p_pair_mode();  // fftq.hip: row pass of a column-parity shard (0: pass A3P)
 hipError_t launch_pass_a_q(const DevView& v, float t, hipStream_t s);
 hipError_t launch_pass_b_q(const DevView& v, hipStream_t s);
 // fft4k.hip with the three-plane intermediate: C1 also forms and transforms R[Q4] into the fourth

@@ -819,6 +819,51 @@ def test_column_parity_shards_vs_oracle():
         ctx.close()
 
 
+_PARITY_SCRIPT = r"""
+import sys, numpy as np
+import ocean_hip as oh
+import oracle as O
+out = sys.argv[1]
+res = []
+for c in (0, 3):
+    for b in (0, 1):
+        ctx = oh.OceanContext(4096, 1, 1)
+        ctx.set_params(O.scene_params(), O.SCENE_CASCADES[c:c + 1])
+        ctx.set_noise(0, O.generate_noise(4096, 20251121))
+        ctx.init_spectrum()
+        ctx.set_column_parity(b)
+        for t in (0.25, 3.0):
+            ctx.step(t)
+        res += [ctx.read(tex)[:, :2048] for tex in (oh.TEX_DISP, oh.TEX_DERIV, oh.TEX_TURB)]
+        ctx.close()
+np.savez(out, *res)
+"""
+
+
+def test_column_parity_row_pass_variants(tmp_path):
+    """The column-parity shard's row pass in its three forms (OCEAN_A3P_PAIR, read once per process):
+    pass A3PP on mirror-pair rows with 1024 lanes (4, the default) and 512 lanes (1), and pass A3P
+    on single rows with full h0 (0).  Their radix orders and factor sharing differ, so they agree
+    within the fp32 tolerance, not bit for bit: cascades 0 and 3, both parities, two frames with foam,
+    every channel at 1e-5 norm-relative against the default (which the oracle test above pins)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env_base = dict(os.environ)
+    env_base["PYTHONPATH"] = os.pathsep.join([os.path.join(root, "ocean-simulation_amd"), os.path.join(root, "oracle"),
+                                              env_base.get("PYTHONPATH", "")])
+    res = {}
+    for val in ("4", "1", "0"):
+        out = str(tmp_path / f"pair_{val}.npz")
+        subprocess.run([sys.executable, "-c", _PARITY_SCRIPT, out], env=dict(env_base, OCEAN_A3P_PAIR=val),
+                       check=True, timeout=200)
+        with np.load(out) as z:
+            res[val] = [z[k] for k in sorted(z.files, key=lambda k: int(k.split("_")[1]))]
+    for val in ("1", "0"):
+        for i, (a, b) in enumerate(zip(res[val], res["4"])):
+            assert_channels(a[None], b[None], what=f"OCEAN_A3P_PAIR={val} texture {i}")
+
+
 def test_column_parity_errors():
     ctx, _ = make_ctx(1024, O.SCENE_CASCADES[:1])
     with pytest.raises(oh.OceanError) as e:
