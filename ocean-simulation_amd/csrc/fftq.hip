@@ -780,9 +780,16 @@ __global__ __launch_bounds__(N / (2 * FIRST)) void k_pass_a3pp(DevView v, float 
             }
             if (b >= 3 && self) return;  // the self-mirror row's duplicate
             const int p = b >= 3 ? b - 3 : b;
-            float2* rowp = v.tplane + (size_t)p * v.inter_stride + ((size_t)u * TILES * N + (b >= 3 ? y2 : y1)) * W;
-            float2* dst = rowp + (size_t)(jj / W) * N * W + (jj % W);
-            dst[(size_t)q * (NSL / W) * N * W] = val;
+            if constexpr (FIRST == 2) {  // 32-bit byte offsets from the intermediate's base (host-checked < 4 GiB)
+                const unsigned e = (unsigned)p * (unsigned)v.inter_stride +
+                                   ((unsigned)u * TILES * N + (unsigned)(b >= 3 ? y2 : y1)) * W +
+                                   (unsigned)(jj / W) * N * W + (unsigned)(jj % W) + (unsigned)q * (NSL / W) * N * W;
+                *(float2*)((char*)v.tplane + (store_off_t)(e * 8u)) = val;
+            } else {
+                float2* rowp = v.tplane + (size_t)p * v.inter_stride + ((size_t)u * TILES * N + (b >= 3 ? y2 : y1)) * W;
+                float2* dst = rowp + (size_t)(jj / W) * N * W + (jj % W);
+                dst[(size_t)q * (NSL / W) * N * W] = val;
+            }
         };
         E::template stages_from<1>(lds, tws, emit, live);
         __syncthreads();
@@ -1005,12 +1012,13 @@ bool pass_q_supported(int n, int planes) {
     return planes == 4 && (n == 512 || n == 1024 || n == 4096 || (n == 2048 && q2048));
 }
 
-// Row pass of a column-parity shard (OCEAN_A3P_PAIR): 4 (default) pass A3PP on 1024 lanes with the
-// next pair's h0k loaded after the stages; 3 the same with it in flight; 1 / 2 pass A3PP on 512 lanes
-// (early / late); 0 pass A3P (one row per item, full h0).  Pass A3PP needs a valid h0k (the caller
-// passes a null h0k after an H0 upload, and pass A3P runs).
+// Row pass of a column-parity shard (OCEAN_A3P_PAIR): 3 (default) pass A3PP on 1024 lanes with the
+// next pair's h0k in flight across the stages (7 VGPRs spilled; 0.094 against 0.098 ms); 4 the same
+// with it loaded after the stages; 1 / 2 pass A3PP on 512 lanes (early / late); 0 pass A3P (one row
+// per item, full h0).  Pass A3PP needs a valid h0k (the caller passes a null h0k after an H0 upload,
+// and pass A3P runs).
 int pass_a3p_pair_mode() {
-    static const int pair = env_int_q("OCEAN_A3P_PAIR", 4);
+    static const int pair = env_int_q("OCEAN_A3P_PAIR", 3);
     return pair;
 }
 
@@ -1023,7 +1031,10 @@ hipError_t launch_pass_a_q(const DevView& v, float t, hipStream_t s) {
         const int pair = pass_a3p_pair_mode();
         if (pair && v.h0k) {
             const int items = v.units * (4096 / 2 + 1);
-            if (pair == 3 || pair == 4) {  // 1024 lanes, radix-2 first stage (early / late next-pair h0k)
+            // 1024 lanes, radix-2 first stage (early / late next-pair h0k); its stores take 32-bit byte
+            // offsets, so the three intermediate planes must lie within 4 GiB of the base (else 512 lanes)
+            const bool off32 = (size_t)v.inter_stride * 3 * 8 < ((size_t)1 << 32);
+            if ((pair == 3 || pair == 4) && off32) {
                 constexpr int T2 = 4096 / 4;
                 if (pair == 4) {
                     const int g = grid_q(k_pass_a3pp<4096, false, 2>, T2, items);
