@@ -281,6 +281,163 @@ __global__ __launch_bounds__(kOpSeq * kOpL1 / kElems) void k_opc2(const float2* 
     }
 }
 
+// ------------------------------------------- folded columns (N = 2048 / 4096)
+// The column transform at N = F L (L = 1024, F = 2 / 4) split by decimation in frequency:
+//   X[F m + b] = sum_{n < L} z_b[n] w_L^(n m),   z_b[n] = w_N^(n b) sum_{r < F} a[n + L r] w_F^(r b).
+// k_rowsf transforms rows n + L r (r < F) of one unit-plane, folds the F results column by column into
+// z_b[n] and stores z_b at row b L + n of the scratch (sub-plane b);
+// k_colsf runs L-point column tiles over the scratch's sub-planes -- the N = 1024 column shape, whose
+// whole columns fit LDS 8 or 16 wide (64 / 128-byte row pieces) -- and writes row F m + b of the plane,
+// permuted.  The 4-column tiles of a whole 4096-point column (32-byte pieces) are not needed.
+constexpr int kFoldL = 1024;
+#ifndef OCEAN_ROWSF_WPEU
+#define OCEAN_ROWSF_WPEU 0  // waves per SIMD k_rowsf is compiled for (0: the compiler's choice; A/B builds)
+#endif
+#if OCEAN_ROWSF_WPEU
+#define ROWSF_WPEU __attribute__((amdgpu_waves_per_eu(OCEAN_ROWSF_WPEU)))
+#else
+#define ROWSF_WPEU
+#endif
+
+// k_rowsf: a one-row engine (N / 16 lanes); item n runs its F rows n + L r back to back, in the order
+// r = 0, 2, 1, 3 (F = 4) or 0, 1 (F = 2), with the next row's loads in flight across each row's stages.
+// A lane's last-stage outputs sit at the same columns x for every row, so the fold is a radix-F
+// butterfly in registers, formed incrementally: (a0 + a2, a0 - a2) after row 2, a1 held, then
+// z_0 = s0 + s1, z_2 = s0 - s1, z_1 = d0 + i d1, z_3 = d0 - i d1 with s1, d1 = a1 +- a3.
+template <int N>
+__global__ __launch_bounds__(N / kElems) ROWSF_WPEU void k_rowsf(const float2* __restrict__ plane, float2* __restrict__ scratch,
+                                                      int items, const float2* __restrict__ tw) {
+    constexpr int F = N / kFoldL, L = kFoldL;
+    static_assert(F == 2 || F == 4, "fold of 2 or 4 rows");
+    using TW = StageTwLds<N>;
+    using E = Engine<N, 1, false, true, 16, TW>;
+    constexpr int T = E::THREADS;
+    static_assert(kElems == E::R0, "one stage-0 butterfly per lane");
+    __shared__ float2 lds[E::LDS_ELEMS];
+    __shared__ float2 twl[TW::kLdsEntries];
+    TW::load(twl, tw, threadIdx.x, T);
+    const float2* tws = TW::table(twl, tw);
+    const int j = (int)threadIdx.x;
+    // sub-step k of item it: row n + L r(k), r = 0, 2, 1, 3 (F = 4) / 0, 1 (F = 2)
+    auto row_of = [&](int it, int k) {
+        const int up = it / L, n = it - up * L;
+        const int r = F == 4 ? ((k & 1) << 1 | (k >> 1)) : k;
+        return (size_t)up * N * N + (size_t)(n + L * r) * N;
+    };
+    auto load = [&](int it, int k, float2 (&d)[kElems]) {
+        const Win w = make_win(plane + row_of(it, k), (unsigned)(N * 8));
+#pragma unroll
+        for (int q = 0; q < kElems; ++q) d[q] = bload2(w, j * 8, q * (N / kElems) * 8);
+    };
+    float2 cur[kElems], nxt[kElems];
+    float2 h0[kElems], h1[kElems], h2[F == 4 ? kElems : 1];
+    int it = blockIdx.x;
+    if (it < items) load(it, 0, cur);
+    __syncthreads();  // twiddle table
+    for (; it < items; it += gridDim.x) {
+        const int up = it / L, n = it - up * L;
+        float2* dst = scratch + (size_t)up * N * N + (size_t)n * N;  // row b L + n holds z_b w_N^(n b)
+        float2 wf[F];
+#pragma unroll
+        for (int b = 1; b < F; ++b) wf[b] = tw[n * b];  // n b < N
+#pragma unroll
+        for (int k = 0; k < F; ++k) {
+            if (k + 1 < F) load(it, k + 1, nxt);
+            else if (it + (int)gridDim.x < items) load(it + gridDim.x, 0, nxt);
+            // the fold runs on each last-stage value as it is emitted; the last row's values complete it
+            auto emit = [&](int m, int q, float2 val) {
+                const int i = m * E::RL + q;
+                if (k == 0) {
+                    h0[i] = val;                        // a0
+                } else if (F == 4 && k == 1) {
+                    h1[i] = csub(h0[i], val);           // d0 = a0 - a2
+                    h0[i] = cadd(h0[i], val);           // s0 = a0 + a2
+                } else if (F == 4 && k == 2) {
+                    h2[i] = val;                        // a1
+                } else {
+                    int bb, jj;
+                    E::template bj<E::RL>(j + m * T, bb, jj);
+                    const int x = jj + q * (N / E::RL);
+                    if constexpr (F == 4) {
+                        const float2 s1 = cadd(h2[i], val), d1 = cmul_i(csub(h2[i], val));
+                        dst[x] = cadd(h0[i], s1);
+                        dst[(size_t)1 * L * N + x] = cmul(cadd(h1[i], d1), wf[1]);
+                        dst[(size_t)2 * L * N + x] = cmul(csub(h0[i], s1), wf[2]);
+                        dst[(size_t)3 * L * N + x] = cmul(csub(h1[i], d1), wf[3]);
+                    } else {
+                        dst[x] = cadd(h0[i], val);
+                        dst[(size_t)L * N + x] = cmul(csub(h0[i], val), wf[1]);
+                    }
+                }
+            };
+            E::run_regs(cur, lds, tws, emit);
+#pragma unroll
+            for (int i = 0; i < kElems; ++i) cur[i] = nxt[i];
+            __syncthreads();  // the image is free for the next row's stage 0
+        }
+    }
+}
+
+// item = (unit-plane, sub-plane b, W-column tile); G > 1 groups the pieces of 16-column tiles on one
+// XCD as k_cols2 does.
+template <int N, int W, int G>
+__global__ __launch_bounds__(W * kFoldL / kElems) void k_colsf(const float2* __restrict__ scratch,
+                                                               float2* __restrict__ plane, int items,
+                                                               const float2* __restrict__ tw) {
+    constexpr int L = kFoldL, F = N / L;
+    using CT = ColTile<L, W>;  // geometry only: lanes, in_dy / out_dy
+    using TW = OpSubTw<L, N>;
+    using E = Engine<L, W, true, Engine<L, W, true, false>::seq_pad_ok(), 16, TW>;
+    static_assert(E::THREADS == CT::T && E::R0 == CT::R0 && E::RL == CT::RL, "tile geometry");
+    constexpr int T = E::THREADS;
+    constexpr int TILES = N / W;  // column tiles per sub-plane
+    __shared__ float2 lds[E::LDS_ELEMS];
+    __shared__ float2 twl[TW::kLdsEntries];
+    TW::load(twl, tw, threadIdx.x, T);
+    const int lb = CT::lane_b(), lj = CT::lane_j();
+    const int voff = (lj * N + lb) * 8;          // input element (lb, n = lj) of a sub-plane tile
+    const int ooff = (F * lj * N + lb) * 8;      // output element (lb, y = F lj) from the tile's row b
+    auto tile_of = [&](int item) {
+        if constexpr (G > 1) return (item & ~(8 * G - 1)) + G * (item & 7) + ((item >> 3) & (G - 1));
+        else return item;
+    };
+    auto decode = [&](int item, int& up, int& b, int& x0) {
+        const int t = tile_of(item);
+        up = t / (F * TILES);
+        const int r = t - up * F * TILES;
+        b = r / TILES;
+        x0 = (r - b * TILES) * W;
+    };
+    float2 cur[kElems], nxt[kElems];
+    auto load = [&](int item, float2 (&d)[kElems]) {
+        int up, b, x0;
+        decode(item, up, b, x0);
+        const size_t o = (size_t)up * N * N + (size_t)b * L * N + x0;
+        const Win w = make_win(scratch + o, (unsigned)(((size_t)L * N - x0) * 8));
+#pragma unroll
+        for (int i = 0; i < kElems; ++i) d[i] = bload2(w, voff, CT::in_dy(i) * N * 8);
+    };
+    int item = blockIdx.x;
+    if (item < items) load(item, cur);
+    __syncthreads();
+    for (; item < items; item += gridDim.x) {
+        const int next = item + gridDim.x;
+        if (next < items) load(next, nxt);
+        int up, b, x0;
+        decode(item, up, b, x0);
+        const Win w = make_win(plane + (size_t)up * N * N + (size_t)b * N + x0, 0);
+        auto emit = [&](int m, int q, float2 val) {
+            const int dy = CT::out_dy(m, q);
+            const float s = perm_sign(x0 + lb, F * (lj + dy) + b);
+            gstore2(make_float2(val.x * s, val.y * s), w, ooff, F * dy * N * 8);
+        };
+        E::run_regs(cur, lds, twl, emit);
+#pragma unroll
+        for (int i = 0; i < kElems; ++i) cur[i] = nxt[i];
+        __syncthreads();
+    }
+}
+
 // --------------------------------------------------------------- launch
 template <class K>
 int persistent_grid(K kernel, int threads, int items) {
@@ -390,6 +547,38 @@ struct Op4 {
     }
 };
 
+// Folded operator for N = 2048 / 4096 over `ups` consecutive unit-planes: part 0 = k_rowsf (planes ->
+// scratch sub-planes), part 1 / 2 = k_colsf on 8 / 16-column tiles (scratch -> planes, permuted).
+template <int N>
+struct OpFold {
+    template <int W, int G>
+    static hipError_t cols(const DevView* v, float2* planes, int ups, const float2* scratch, hipStream_t s) {
+        constexpr int T = W * kFoldL / kElems;
+        const int items = ups * (N / kFoldL) * (N / W);
+        int g = persistent_grid(k_colsf<N, W, G>, T, items);
+        if (G > 1) g -= g % (8 * G);
+        launch((k_colsf<N, W, G>), dim3(g), dim3(T), 0, s, scratch, planes, items, v->tw);
+        return hipGetLastError();
+    }
+    static hipError_t go(const DevView* v, float2* planes, int ups, float2* scratch, int part, hipStream_t s) {
+        if constexpr (N != 2048 && N != 4096) {
+            return hipErrorInvalidValue;
+        } else {
+            if (part == 0) {
+                constexpr int T = N / kElems;
+                const int items = ups * kFoldL;
+                const int g = persistent_grid(k_rowsf<N>, T, items);
+                launch((k_rowsf<N>), dim3(g), dim3(T), 0, s, (const float2*)planes, scratch, items, v->tw);
+                return hipGetLastError();
+            }
+            // part 1: 8-column halves of 16-column tiles paired on one XCD (k_cols2 at N = 1024);
+            // part 2: whole 16-column tiles (A/B, OCEAN_FOLD_COLS=16)
+            if (part == 2) return cols<16, 1>(v, planes, ups, scratch, s);
+            return cols<8, 2>(v, planes, ups, scratch, s);
+        }
+    }
+};
+
 template <int N>
 struct StageTwCount {
     static hipError_t go(size_t* out) {
@@ -416,6 +605,11 @@ hipError_t launch_ifft_cols_v2(const DevView& v, float2* base, int ups, hipStrea
 hipError_t launch_ifft_four_step(const DevView& v, float2* planes, int ups, float2* scratch, int part, hipStream_t s) {
     if (v.n != 2048 && v.n != 4096) return hipErrorInvalidValue;
     return v.n == 2048 ? Op4<2048>::go(&v, planes, ups, scratch, part, s) : Op4<4096>::go(&v, planes, ups, scratch, part, s);
+}
+hipError_t launch_ifft_fold(const DevView& v, float2* planes, int ups, float2* scratch, int part, hipStream_t s) {
+    if (v.n != 2048 && v.n != 4096) return hipErrorInvalidValue;
+    return v.n == 2048 ? OpFold<2048>::go(&v, planes, ups, scratch, part, s)
+                       : OpFold<4096>::go(&v, planes, ups, scratch, part, s);
 }
 
 }  // namespace ocean

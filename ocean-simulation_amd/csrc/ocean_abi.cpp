@@ -152,6 +152,9 @@ struct ocean_ctx {
     int chunk_min = 1 << 30; // OCEAN_CHUNK_MIN: units per chunk when one unit exceeds OCEAN_CHUNK_MIB
     int chunk_reuse = 1;     // OCEAN_CHUNK_REUSE=0: one intermediate region per unit (A/B)
     int op_four_step = 0;    // OCEAN_OP_FOUR_STEP=1: ocean_ifft2d at N >= 2048 through four-step columns (A/B)
+    int op_fold = -1;        // OCEAN_OP_FOLD: ocean_ifft2d at N >= 2048 through folded 1024-point columns
+                             // (-1 auto: N = 4096; 0 off: XCD-grouped whole-column tiles; 1 on at 2048 too)
+    int op_fold_cols = 8;    // OCEAN_FOLD_COLS: column-tile width of the folded columns (8 paired, or 16; A/B)
     long op_chunk_mib = 0;   // OCEAN_OP_CHUNK_MIB: MiB of unit-planes per chunk of the operator IFFT (0: auto)
     size_t inter_units = 0;  // units the intermediate holds (a chunk's, or all with chunk_reuse = 0)
     int band_x0 = 0, band_nx = 0;  // column band of the fused passes (ocean_set_column_band); nx = n: whole
@@ -432,6 +435,8 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
     if (const char* km = std::getenv("OCEAN_CHUNK_MIN")) c->chunk_min = std::max(1, std::atoi(km));
     if (const char* kr = std::getenv("OCEAN_CHUNK_REUSE")) c->chunk_reuse = std::atoi(kr);
     if (const char* kf = std::getenv("OCEAN_OP_FOUR_STEP")) c->op_four_step = std::atoi(kf);
+    if (const char* kd = std::getenv("OCEAN_OP_FOLD")) c->op_fold = std::atoi(kd);
+    if (const char* kw = std::getenv("OCEAN_FOLD_COLS")) c->op_fold_cols = std::atoi(kw);
     if (const char* kg = std::getenv("OCEAN_GRAPH")) c->graph_mode = std::atoi(kg);
     if (const char* ko = std::getenv("OCEAN_OP_CHUNK_MIB")) c->op_chunk_mib = std::max(0L, std::atol(ko));
     // Width of the fused path's column tiles.  With fewer tiles than CUs (one 512^2
@@ -669,6 +674,33 @@ int ocean_ifft2d(ocean_ctx* ctx, int plane_mask) {
                 if (int r = timed(ctx, 1, [&] {
                         hipError_t e = ocean::launch_ifft_four_step(v, planes, kc, ctx->tplane, 1, ctx->stream);
                         return e != hipSuccess ? e : ocean::launch_ifft_four_step(v, planes, kc, ctx->tplane, 2, ctx->stream);
+                    }, "ifft_cols"))
+                    return r;
+            }
+            p += np;
+            continue;
+        }
+        if (ctx->n >= 2048 && (ctx->op_fold > 0 || (ctx->op_fold < 0 && ctx->n == 4096))) {
+            // Folded columns (fft2.hip k_rowsf / k_colsf): per chunk of unit-planes, rows + the
+            // decimation-in-frequency fold planes -> scratch sub-planes, then 1024-point column tiles
+            // scratch -> planes; a chunk of at most OCEAN_OP_CHUNK_MIB stays in the Infinity
+            // Cache between the two launches (auto 128 MiB: both launches are out of place, so a chunk
+            // occupies twice its size; 4 x 4096^2 x 4 planes, columns 256 / 128 / 64 MiB: 0.44 / 0.71 / 0.71)
+            const int ups = np * (int)ctx->units();
+            const size_t scratch_ups = ctx->inter_units * ctx->P;
+            const long mib = ctx->op_chunk_mib > 0 ? ctx->op_chunk_mib : 128;
+            int k = (int)std::max<size_t>(1, ((size_t)mib << 20) / (up_elems * 8));
+            k = (int)std::min<size_t>((size_t)k, scratch_ups);
+            for (int c0 = 0; c0 < ups; c0 += k) {
+                const int kc = std::min(k, ups - c0);
+                float2* planes = ctx->plane[p] + (size_t)c0 * up_elems;
+                if (int r = timed(ctx, 0, [&] {
+                        return ocean::launch_ifft_fold(v, planes, kc, ctx->tplane, 0, ctx->stream);
+                    }, "ifft_rows"))
+                    return r;
+                if (int r = timed(ctx, 1, [&] {
+                        return ocean::launch_ifft_fold(v, planes, kc, ctx->tplane, ctx->op_fold_cols == 16 ? 2 : 1,
+                                                       ctx->stream);
                     }, "ifft_cols"))
                     return r;
             }

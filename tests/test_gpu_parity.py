@@ -102,15 +102,30 @@ def test_ifft2d_operator_vs_oracle(n):
     ctx.close()
 
 
-@pytest.mark.parametrize("n,C,mask,four_step", [(2048, 1, 0b0001, False), (4096, 4, 0b1111, False),
-                                                 (2048, 1, 0b0001, True), (4096, 4, 0b1111, True)])
-def test_ifft2d_operator_large_vs_numpy(n, C, mask, four_step, monkeypatch):
+# operator schedules at N >= 2048 (ocean_ifft2d, ocean_abi.cpp): the default (folded columns at 4096,
+# XCD-grouped whole-column tiles at 2048), and the A/B knobs, read at ocean_create
+OP_MODES = {
+    "default": {},
+    "fold": {"OCEAN_OP_FOLD": "1"},                            # folded columns at 2048 too
+    "fold16": {"OCEAN_OP_FOLD": "1", "OCEAN_FOLD_COLS": "16"},  # folded columns on 16-column tiles
+    "grouped": {"OCEAN_OP_FOLD": "0"},                         # whole-column tiles grouped on one XCD
+    "four_step": {"OCEAN_OP_FOUR_STEP": "1"},
+}
+
+
+@pytest.mark.parametrize("n,C,mask,mode", [(2048, 1, 0b0001, "default"), (4096, 4, 0b1111, "default"),
+                                           (2048, 1, 0b0001, "fold"), (4096, 1, 0b0110, "fold16"),
+                                           (4096, 4, 0b1111, "grouped"), (4096, 2, 0b1001, "fold"),
+                                           (2048, 1, 0b0001, "four_step"),
+                                           (4096, 4, 0b1111, "four_step")])
+def test_ifft2d_operator_large_vs_numpy(n, C, mask, mode, monkeypatch):
     """The operator at N = 2048 / 4096 on every requested plane of every cascade, against numpy's
-    float64 ifft2 (ref64); 4 x 4096^2 x 4 planes is cfg5's whole plane set (2 GiB).  Default: in-place
-    rows, then whole-column tiles grouped on one XCD, two unit-planes per chunk at 4096 (fft2.hip
-    Cols2); four_step: the A/B four-step column passes through the scratch (OCEAN_OP_FOUR_STEP=1)."""
-    if four_step:
-        monkeypatch.setenv("OCEAN_OP_FOUR_STEP", "1")
+    float64 ifft2 (ref64); 4 x 4096^2 x 4 planes is cfg5's whole plane set (2 GiB).  Default at 4096:
+    rows + decimation-in-frequency fold into the scratch, then 1024-point column tiles (fft2.hip
+    k_rowsf / k_colsf); at 2048 in-place rows, then whole-column tiles grouped on one XCD (Cols2); the
+    other OP_MODES are the A/B schedules."""
+    for k, val in OP_MODES[mode].items():
+        monkeypatch.setenv(k, val)
     ctx = oh.OceanContext(n, C, 1)
     planes = [p for p in range(4) if mask >> p & 1]
 
@@ -121,24 +136,29 @@ def test_ifft2d_operator_large_vs_numpy(n, C, mask, four_step, monkeypatch):
         for c in range(C):
             ctx.write(oh.TEX_PLANE0 + p, slice_data(p, c), 0, c)
     ctx.ifft2d(mask)
-    for p in planes:
+    for p in range(4):
         for c in range(C):
-            got = cplx(ctx.read(oh.TEX_PLANE0 + p, 0, c))
+            got = ctx.read(oh.TEX_PLANE0 + p, 0, c)
+            if p not in planes:
+                if c == 0 and p == 0:
+                    assert not np.any(got), "plane outside the mask written"
+                continue
             want = O.ref64.ifft2d(cplx(slice_data(p, c)[None]))[0]
-            e = O.rel_err(got, want)
+            e = O.rel_err(cplx(got), want)
             assert e <= 2e-6, f"plane {p} cascade {c}: {e:.2e}"
     ctx.close()
 
 
-@pytest.mark.parametrize("chunk_mib,four_step", [(None, False), (64, False), (None, True), (64, True)])
-def test_ifft2d_operator_2048_vs_oracle(chunk_mib, four_step, monkeypatch):
+@pytest.mark.parametrize("chunk_mib,mode", [(None, "default"), (64, "default"), (None, "four_step"),
+                                            (64, "four_step"), (None, "fold"), (64, "fold"), (32, "fold16")])
+def test_ifft2d_operator_2048_vs_oracle(chunk_mib, mode, monkeypatch):
     """N = 2048 operator against the reference's radix-2 schedule (oracle) on three planes of two
-    cascades (6 unit-planes of 32 MiB): one chunk by default, or 3 chunks of 2 unit-planes at
-    OCEAN_OP_CHUNK_MIB=64; plane 3 untouched; default and four-step (OCEAN_OP_FOUR_STEP=1) columns."""
+    cascades (6 unit-planes of 32 MiB): one chunk by default, or 3 / 6 chunks at OCEAN_OP_CHUNK_MIB=64 /
+    32; plane 3 untouched; every OP_MODES schedule."""
     if chunk_mib:
         monkeypatch.setenv("OCEAN_OP_CHUNK_MIB", str(chunk_mib))
-    if four_step:
-        monkeypatch.setenv("OCEAN_OP_FOUR_STEP", "1")
+    for k, val in OP_MODES[mode].items():
+        monkeypatch.setenv(k, val)
     n, C = 2048, 2
     ctx = oh.OceanContext(n, C, 1)
     rng = np.random.default_rng(7)
