@@ -282,7 +282,7 @@ __global__ __launch_bounds__(kOpSeq * kOpL1 / kElems) void k_opc2(const float2* 
 }
 
 // ------------------------------------------- folded columns (N = 2048 / 4096)
-// The column transform at N = F L (L = 1024, F = 2 / 4) split by decimation in frequency:
+// The column transform at N = F L (F = 2 / 4) split by decimation in frequency:
 //   X[F m + b] = sum_{n < L} z_b[n] w_L^(n m),   z_b[n] = w_N^(n b) sum_{r < F} a[n + L r] w_F^(r b).
 // k_rowsf transforms rows n + L r (r < F) of one unit-plane, folds the F results column by column into
 // z_b[n] and stores z_b at row b L + n of the scratch (sub-plane b);
@@ -304,10 +304,10 @@ constexpr int kFoldL = 1024;
 // A lane's last-stage outputs sit at the same columns x for every row, so the fold is a radix-F
 // butterfly in registers, formed incrementally: (a0 + a2, a0 - a2) after row 2, a1 held, then
 // z_0 = s0 + s1, z_2 = s0 - s1, z_1 = d0 + i d1, z_3 = d0 - i d1 with s1, d1 = a1 +- a3.
-template <int N>
+template <int N, int F>
 __global__ __launch_bounds__(N / kElems) ROWSF_WPEU void k_rowsf(const float2* __restrict__ plane, float2* __restrict__ scratch,
                                                       int items, const float2* __restrict__ tw) {
-    constexpr int F = N / kFoldL, L = kFoldL;
+    constexpr int L = N / F;
     static_assert(F == 2 || F == 4, "fold of 2 or 4 rows");
     using TW = StageTwLds<N>;
     using E = Engine<N, 1, false, true, 16, TW>;
@@ -380,11 +380,11 @@ __global__ __launch_bounds__(N / kElems) ROWSF_WPEU void k_rowsf(const float2* _
 
 // item = (unit-plane, sub-plane b, W-column tile); G > 1 groups the pieces of 16-column tiles on one
 // XCD as k_cols2 does.
-template <int N, int W, int G>
-__global__ __launch_bounds__(W * kFoldL / kElems) void k_colsf(const float2* __restrict__ scratch,
-                                                               float2* __restrict__ plane, int items,
-                                                               const float2* __restrict__ tw) {
-    constexpr int L = kFoldL, F = N / L;
+template <int N, int F, int W, int G>
+__global__ __launch_bounds__(W * (N / F) / kElems) void k_colsf(const float2* __restrict__ scratch,
+                                                                float2* __restrict__ plane, int items,
+                                                                const float2* __restrict__ tw) {
+    constexpr int L = N / F;
     using CT = ColTile<L, W>;  // geometry only: lanes, in_dy / out_dy
     using TW = OpSubTw<L, N>;
     using E = Engine<L, W, true, Engine<L, W, true, false>::seq_pad_ok(), 16, TW>;
@@ -551,30 +551,43 @@ struct Op4 {
 // scratch sub-planes), part 1 / 2 = k_colsf on 8 / 16-column tiles (scratch -> planes, permuted).
 template <int N>
 struct OpFold {
-    template <int W, int G>
+    template <int F, int W, int G>
     static hipError_t cols(const DevView* v, float2* planes, int ups, const float2* scratch, hipStream_t s) {
-        constexpr int T = W * kFoldL / kElems;
-        const int items = ups * (N / kFoldL) * (N / W);
-        int g = persistent_grid(k_colsf<N, W, G>, T, items);
+        constexpr int T = W * (N / F) / kElems;
+        const int items = ups * F * (N / W);
+        int g = persistent_grid(k_colsf<N, F, W, G>, T, items);
         if (G > 1) g -= g % (8 * G);
-        launch((k_colsf<N, W, G>), dim3(g), dim3(T), 0, s, scratch, planes, items, v->tw);
+        launch((k_colsf<N, F, W, G>), dim3(g), dim3(T), 0, s, scratch, planes, items, v->tw);
         return hipGetLastError();
     }
-    static hipError_t go(const DevView* v, float2* planes, int ups, float2* scratch, int part, hipStream_t s) {
-        if constexpr (N != 2048 && N != 4096) {
-            return hipErrorInvalidValue;
-        } else {
-            if (part == 0) {
-                constexpr int T = N / kElems;
-                const int items = ups * kFoldL;
-                const int g = persistent_grid(k_rowsf<N>, T, items);
-                launch((k_rowsf<N>), dim3(g), dim3(T), 0, s, (const float2*)planes, scratch, items, v->tw);
-                return hipGetLastError();
+    template <int F>
+    static hipError_t rows(const DevView* v, float2* planes, int ups, float2* scratch, hipStream_t s) {
+        constexpr int T = N / kElems;
+        const int items = ups * (N / F);
+        const int g = persistent_grid(k_rowsf<N, F>, T, items);
+        launch((k_rowsf<N, F>), dim3(g), dim3(T), 0, s, (const float2*)planes, scratch, items, v->tw);
+        return hipGetLastError();
+    }
+    static hipError_t go(const DevView* v, float2* planes, int ups, float2* scratch, int part, int fold,
+                         hipStream_t s) {
+        if constexpr (N == 2048) {
+            if (fold != 2) return hipErrorInvalidValue;
+            if (part == 0) return rows<2>(v, planes, ups, scratch, s);
+            if (part == 2) return cols<2, 16, 1>(v, planes, ups, scratch, s);
+            return cols<2, 8, 2>(v, planes, ups, scratch, s);
+        } else if constexpr (N == 4096) {
+            if (fold == 2) {  // 2048-point columns: 8-column halves paired on one XCD (the N = 2048 shape)
+                if (part == 0) return rows<2>(v, planes, ups, scratch, s);
+                return cols<2, 8, 2>(v, planes, ups, scratch, s);
             }
+            if (fold != 4) return hipErrorInvalidValue;
+            if (part == 0) return rows<4>(v, planes, ups, scratch, s);
             // part 1: 8-column halves of 16-column tiles paired on one XCD (k_cols2 at N = 1024);
             // part 2: whole 16-column tiles (A/B, OCEAN_FOLD_COLS=16)
-            if (part == 2) return cols<16, 1>(v, planes, ups, scratch, s);
-            return cols<8, 2>(v, planes, ups, scratch, s);
+            if (part == 2) return cols<4, 16, 1>(v, planes, ups, scratch, s);
+            return cols<4, 8, 2>(v, planes, ups, scratch, s);
+        } else {
+            return hipErrorInvalidValue;
         }
     }
 };
@@ -606,10 +619,11 @@ hipError_t launch_ifft_four_step(const DevView& v, float2* planes, int ups, floa
     if (v.n != 2048 && v.n != 4096) return hipErrorInvalidValue;
     return v.n == 2048 ? Op4<2048>::go(&v, planes, ups, scratch, part, s) : Op4<4096>::go(&v, planes, ups, scratch, part, s);
 }
-hipError_t launch_ifft_fold(const DevView& v, float2* planes, int ups, float2* scratch, int part, hipStream_t s) {
+hipError_t launch_ifft_fold(const DevView& v, float2* planes, int ups, float2* scratch, int part, int fold,
+                            hipStream_t s) {
     if (v.n != 2048 && v.n != 4096) return hipErrorInvalidValue;
-    return v.n == 2048 ? OpFold<2048>::go(&v, planes, ups, scratch, part, s)
-                       : OpFold<4096>::go(&v, planes, ups, scratch, part, s);
+    return v.n == 2048 ? OpFold<2048>::go(&v, planes, ups, scratch, part, fold, s)
+                       : OpFold<4096>::go(&v, planes, ups, scratch, part, fold, s);
 }
 
 }  // namespace ocean

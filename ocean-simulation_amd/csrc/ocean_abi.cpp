@@ -155,6 +155,7 @@ struct ocean_ctx {
     int op_fold = -1;        // OCEAN_OP_FOLD: ocean_ifft2d at N >= 2048 through folded 1024-point columns
                              // (-1 auto: N = 4096; 0 off: XCD-grouped whole-column tiles; 1 on at 2048 too)
     int op_fold_cols = 8;    // OCEAN_FOLD_COLS: column-tile width of the folded columns (8 paired, or 16; A/B)
+    int op_fold_f = 2;       // OCEAN_FOLD_F: rows folded per column at 4096 (2: 2048-point columns, 4: 1024-point)
     long op_chunk_mib = 0;   // OCEAN_OP_CHUNK_MIB: MiB of unit-planes per chunk of the operator IFFT (0: auto)
     size_t inter_units = 0;  // units the intermediate holds (a chunk's, or all with chunk_reuse = 0)
     int band_x0 = 0, band_nx = 0;  // column band of the fused passes (ocean_set_column_band); nx = n: whole
@@ -437,6 +438,7 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
     if (const char* kf = std::getenv("OCEAN_OP_FOUR_STEP")) c->op_four_step = std::atoi(kf);
     if (const char* kd = std::getenv("OCEAN_OP_FOLD")) c->op_fold = std::atoi(kd);
     if (const char* kw = std::getenv("OCEAN_FOLD_COLS")) c->op_fold_cols = std::atoi(kw);
+    if (const char* kf2 = std::getenv("OCEAN_FOLD_F")) c->op_fold_f = std::atoi(kf2) == 4 ? 4 : 2;
     if (const char* kg = std::getenv("OCEAN_GRAPH")) c->graph_mode = std::atoi(kg);
     if (const char* ko = std::getenv("OCEAN_OP_CHUNK_MIB")) c->op_chunk_mib = std::max(0L, std::atol(ko));
     // Width of the fused path's column tiles.  With fewer tiles than CUs (one 512^2
@@ -694,13 +696,14 @@ int ocean_ifft2d(ocean_ctx* ctx, int plane_mask) {
             for (int c0 = 0; c0 < ups; c0 += k) {
                 const int kc = std::min(k, ups - c0);
                 float2* planes = ctx->plane[p] + (size_t)c0 * up_elems;
+                const int fold = ctx->n == 2048 ? 2 : ctx->op_fold_f;
                 if (int r = timed(ctx, 0, [&] {
-                        return ocean::launch_ifft_fold(v, planes, kc, ctx->tplane, 0, ctx->stream);
+                        return ocean::launch_ifft_fold(v, planes, kc, ctx->tplane, 0, fold, ctx->stream);
                     }, "ifft_rows"))
                     return r;
                 if (int r = timed(ctx, 1, [&] {
-                        return ocean::launch_ifft_fold(v, planes, kc, ctx->tplane, ctx->op_fold_cols == 16 ? 2 : 1,
-                                                       ctx->stream);
+                        const int part = ctx->op_fold_cols == 16 && fold == 4 ? 2 : 1;
+                        return ocean::launch_ifft_fold(v, planes, kc, ctx->tplane, part, fold, ctx->stream);
                     }, "ifft_cols"))
                     return r;
             }

@@ -113,11 +113,12 @@ hipError_t launch_ifft_cols_v2(const DevView& v, float2* base, int ups, hipStrea
 // unit-plane p * U + u) through `scratch`; part 0 = rows (planes -> scratch), 1 = four-step column
 // step 1 (in place on scratch), 2 = step 2 + permute (scratch -> planes).
 hipError_t launch_ifft_four_step(const DevView& v, float2* planes, int ups, float2* scratch, int part, hipStream_t s);
-// N = 2048 / 4096, the default operator: the column transform split by decimation in frequency into
-// F = N / 1024 column transforms of 1024 points (fft2.hip k_rowsf / k_colsf); part 0 = rows + fold
-// (planes -> scratch sub-planes), 1 = 1024-point columns + permute (scratch -> planes) on XCD-paired
-// 8-column tiles, 2 = the same on 16-column tiles (A/B).
-hipError_t launch_ifft_fold(const DevView& v, float2* planes, int ups, float2* scratch, int part, hipStream_t s);
+// N = 2048 / 4096: the operator's column transform split by decimation in frequency into `fold` (2 or 4)
+// column transforms of N / fold points (fft2.hip k_rowsf / k_colsf); part 0 = rows + fold (planes ->
+// scratch sub-planes), 1 = the column transforms + permute (scratch -> planes) on XCD-paired 8-column
+// tiles, 2 = the same on 16-column tiles (A/B; fold 4 at 4096, or 2 at 2048).
+hipError_t launch_ifft_fold(const DevView& v, float2* planes, int ups, float2* scratch, int part, int fold,
+                            hipStream_t s);
 
 // fft3.hip: fused frame through the tile-major intermediate; the row pass
 // recomputes wave data and feeds evolve straight into a radix-4/8 first stage;

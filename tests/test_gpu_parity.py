@@ -109,13 +109,16 @@ OP_MODES = {
     "fold": {"OCEAN_OP_FOLD": "1"},                            # folded columns at 2048 too
     "fold16": {"OCEAN_OP_FOLD": "1", "OCEAN_FOLD_COLS": "16"},  # folded columns on 16-column tiles
     "grouped": {"OCEAN_OP_FOLD": "0"},                         # whole-column tiles grouped on one XCD
+    "fold2": {"OCEAN_FOLD_F": "2"},                            # at 4096: two rows folded, 2048-point columns
+    "fold4": {"OCEAN_FOLD_F": "4"},                            # at 4096: four rows folded, 1024-point columns
     "four_step": {"OCEAN_OP_FOUR_STEP": "1"},
 }
 
 
 @pytest.mark.parametrize("n,C,mask,mode", [(2048, 1, 0b0001, "default"), (4096, 4, 0b1111, "default"),
                                            (2048, 1, 0b0001, "fold"), (4096, 1, 0b0110, "fold16"),
-                                           (4096, 4, 0b1111, "grouped"), (4096, 2, 0b1001, "fold"),
+                                           (4096, 4, 0b1111, "grouped"), (4096, 2, 0b1001, "fold2"),
+                                           (4096, 2, 0b1001, "fold4"),
                                            (2048, 1, 0b0001, "four_step"),
                                            (4096, 4, 0b1111, "four_step")])
 def test_ifft2d_operator_large_vs_numpy(n, C, mask, mode, monkeypatch):
