@@ -35,6 +35,9 @@
 #ifndef OCEAN_AQ_SHARE
 #define OCEAN_AQ_SHARE 0  // 1: pass AQ also exchanges the in-row mirror texels' factors through LDS (A/B builds)
 #endif
+#ifndef OCEAN_AQ_WST
+#define OCEAN_AQ_WST 1  // pass AQ's intermediate stores: scalar unit base + 32-bit lane offsets (0: 64-bit addresses; A/B)
+#endif
 #ifndef AQ_SKIP
 #define AQ_SKIP 1  // pass AQ's idle pass-1 waves skip the stages (A/B builds)
 #endif
@@ -194,6 +197,9 @@ __global__ __launch_bounds__(N / 4) AQ_WPEU void k_pass_aq(DevView v, float time
         rows_of(it, u, y1, y2);
         const WaveBand wb = band[(u + v.c0) % v.C];
         const bool self = (y1 == y2);
+#if OCEAN_AQ_WST
+        const Win wunit = make_win(v.tplane + (size_t)u * TILES * N * W, 0);
+#endif
 #if OCEAN_AQ_SHARE
         float4 own[2];
 #pragma unroll
@@ -278,9 +284,17 @@ __global__ __launch_bounds__(N / 4) AQ_WPEU void k_pass_aq(DevView v, float time
                     return;
                 }
                 if (BAND && (unsigned)(x - v.x0) >= (unsigned)v.nx) return;  // outside the column band
+#if OCEAN_AQ_WST
+                // scalar unit base + a 32-bit lane offset (plane, row, tile, column; < 4 GiB, host-checked):
+                // one 32-bit add per store instead of a 64-bit address
+                const unsigned off = (unsigned)p * (unsigned)(v.inter_stride * 8) +
+                                     (unsigned)((((s ? y2 : y1) * W) + (jj / W) * N * W + (jj % W)) * 8);
+                gstore2(val, wunit, (int)off, q * (NSL / W) * N * W * 8);
+#else
                 float2* dst = v.tplane + (size_t)p * v.inter_stride + ((size_t)u * TILES * N + (s ? y2 : y1)) * W +
                               (size_t)(jj / W) * N * W + (jj % W);
                 dst[(size_t)q * (NSL / W) * N * W] = val;
+#endif
             };
             // pass 1: sequence slots 2, 3 idle, their butterflies skipped (at N = 1024 the stages are
             // wave-private, wave w = sequence w: waves 2, 3 skip them whole)
