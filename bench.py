@@ -470,8 +470,10 @@ def main():
         # operator-level stage (IFFT.InverseFastFourierTransform x 4 planes), unfused kernels, on the
         # frame's own planes (ocean_evolve before every call): the fused frame never writes them, and
         # zero-filled planes run at a higher clock (MI355X_MICROARCH.md) -- rounds 1-2 timed zeros
+        # PMC records of the operator's kernels: cfg3's (tools/profile.sh) and the 4 x 4096^2 operator's
+        # (profiles/r03zzz_op4k, config "op4k": the same launches per unit-plane chunk as cfg5's)
         ifft_stage = ifft_measure(ctx, max(20, args.steps // 5), "ifft_kernel_stats.csv",
-                                  "cfg3" if args.config == "cfg3" else None)
+                                  {"cfg3": "cfg3", "cfg5": "op4k"}.get(args.config))
         ifft_stage["data"] = "freshly evolved planes before every call (frame data)"
         if rank == 0 and world == 1 and args.config == "cfg3" and not args.no_beyond_cache:
             ifft_stage["beyond_cache"] = ifft_beyond_cache()
