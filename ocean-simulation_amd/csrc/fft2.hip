@@ -286,10 +286,10 @@ __global__ __launch_bounds__(kOpSeq * kOpL1 / kElems) void k_opc2(const float2* 
 //   X[F m + b] = sum_{n < L} z_b[n] w_L^(n m),   z_b[n] = w_N^(n b) sum_{r < F} a[n + L r] w_F^(r b).
 // k_rowsf transforms rows n + L r (r < F) of one unit-plane, folds the F results column by column into
 // z_b[n] and stores z_b at row b L + n of the scratch (sub-plane b);
-// k_colsf runs L-point column tiles over the scratch's sub-planes -- the N = 1024 column shape, whose
-// whole columns fit LDS 8 or 16 wide (64 / 128-byte row pieces) -- and writes row F m + b of the plane,
-// permuted.  The 4-column tiles of a whole 4096-point column (32-byte pieces) are not needed.
-constexpr int kFoldL = 1024;
+// k_colsf runs L-point column tiles over the scratch's sub-planes -- the N = 2048 column shape at F = 2
+// (8-column halves, XCD-paired: 64-byte pieces of 128-byte lines), the N = 1024 one at F = 4 (8 or 16
+// wide) -- and writes row F m + b of the plane, permuted.  The 4-column tiles of a whole 4096-point
+// column (32-byte pieces) are not needed.  At 4096 the default is F = 2 (ocean_abi.cpp, OCEAN_FOLD_F).
 #ifndef OCEAN_ROWSF_WPEU
 #define OCEAN_ROWSF_WPEU 0  // waves per SIMD k_rowsf is compiled for (0: the compiler's choice; A/B builds)
 #endif
