@@ -69,63 +69,90 @@ def algorithmic_bytes(ctx):
     return {"pass_a": a, "pass_b": b, "frame": a + b, "cache_resident": resident}
 
 
-ROUND = "r03"  # profiles/<ROUND>*/ hold this round's profiler records and micro-benchmarks
+def _current_round(root=ROOT):
+    """This round's tag: one past the newest BENCH_rNN.json the driver has recorded (r04 while
+    BENCH_r03.json is the newest), so profiles/<ROUND>* never needs editing between rounds."""
+    import re
+    done = [int(m.group(1)) for f in os.listdir(root) for m in [re.match(r"BENCH_r(\d+)\.json$", f)] if m]
+    return f"r{(max(done) + 1 if done else 1):02d}"
+
+
+ROUND = _current_round()  # profiles/<ROUND>*/ hold this round's micro-benchmark records
+PROFILES = os.path.join(ROOT, "profiles")
 
 
 def _norm(sym):
     return " ".join(sym.split()) if sym else sym
 
 
-def pmc_traffic(symbol, config, profiles_dir=os.path.join(ROOT, "profiles")):
-    """HBM bytes per launch of the kernel `symbol` (the exact demangled name of the kernel that ran,
-    ocean_kernel_name) from the newest committed rocprofv3 PMC summary of `config`
-    (tools/profile.sh -> profiles/<tag>/pmc_summary.json): 2 x FETCH_SIZE (gfx950 reports half of
-    wide streaming reads) + WRITE_SIZE.  (bytes, source dir) or None if no summary holds that
-    symbol."""
-    best = None
+_IDENT = {}
+
+
+def library_identity():
+    """sha256 of the liboceanhip.so this process loaded and of the library's sources (tools/stamp.py)."""
+    if not _IDENT:
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import stamp as st
+        _IDENT.update(lib=st.lib_sha(oh.LIB_PATH), src=st.src_sha())
+    return _IDENT
+
+
+def find_record(config, symbol, profiles_dir=PROFILES):
+    """The committed rocprofv3 record of `config` that holds the kernel `symbol` (the exact demangled
+    name of the kernel that ran, ocean_kernel_name): profiles/<tag>/ with stamp.json (tools/profile.sh +
+    tools/pmc_summary.py), kernel_stats.csv and pmc_summary.json.  Among those, the one whose stamp
+    matches the loaded library's sha256, else its sources' sha256, else the newest stamp (UTC) -- never
+    a directory-name order.  Unstamped directories (before round 4) are not considered.  Returns
+    {dir, avg_us, launches, traffic_bytes_per_launch, match, utc} or None."""
+    import csv
     if not symbol or not os.path.isdir(profiles_dir):
         return None
-    want = _norm(symbol)
-    for d in sorted(os.listdir(profiles_dir)):
-        f = os.path.join(profiles_dir, d, "pmc_summary.json")
-        if not os.path.exists(f):
+    want, ident = _norm(symbol), library_identity()
+    best, best_key = None, None
+    for d in os.listdir(profiles_dir):
+        sp = os.path.join(profiles_dir, d, "stamp.json")
+        ks = os.path.join(profiles_dir, d, "kernel_stats.csv")
+        if not (os.path.exists(sp) and os.path.exists(ks)):
             continue
         try:
-            summ = json.load(open(f))
+            stamp = json.load(open(sp))
         except Exception:
             continue
-        if summ.get("config") != config:
+        if stamp.get("config") != config:
             continue
-        for k, rec in summ.get("kernels", {}).items():
-            if _norm(k) == want:
-                best = (rec["hbm_bytes_per_launch"], d)
-    return best
-
-
-def rocprof_kernel_us(csv_name, symbol, profiles_dir=os.path.join(ROOT, "profiles")):
-    """(average ns -> us, source) of the kernel `symbol` (exact demangled name) from the newest
-    committed rocprofv3 --stats summary named `csv_name` under profiles/<tag>/; None if absent."""
-    import csv
-    best = None
-    if not symbol or not os.path.isdir(profiles_dir):
-        return None
-    want = _norm(symbol)
-    for d in sorted(os.listdir(profiles_dir)):
-        f = os.path.join(profiles_dir, d, csv_name)
-        if not os.path.exists(f):
+        row = next((r for r in csv.DictReader(open(ks)) if _norm(r["Name"]) == want), None)
+        if row is None:
             continue
-        for row in csv.DictReader(open(f)):
-            if _norm(row["Name"]) == want:
-                best = (float(row["AverageNs"]) / 1e3, f"profiles/{d}/{csv_name}")
+        match = "lib" if stamp.get("lib_sha256") == ident["lib"] else (
+            "src" if stamp.get("src_sha256") == ident["src"] else "none")
+        key = ({"lib": 2, "src": 1, "none": 0}[match], stamp.get("utc", ""))
+        if best_key is not None and key <= best_key:
+            continue
+        traffic = None
+        pp = os.path.join(profiles_dir, d, "pmc_summary.json")
+        if os.path.exists(pp):
+            rec = next((v for k, v in json.load(open(pp)).get("kernels", {}).items() if _norm(k) == want), None)
+            traffic = rec["hbm_bytes_per_launch"] if rec else None
+        best_key = key
+        best = {"dir": f"profiles/{d}", "avg_us": float(row["AverageNs"]) / 1e3, "launches": int(row["Calls"]),
+                "traffic_bytes_per_launch": traffic, "match": match, "utc": stamp.get("utc"),
+                "git_head": stamp.get("git_head")}
     return best
 
 
 def _round_dirs(profiles_dir):
-    """This round's profile directories (profiles/<ROUND>*), oldest first: micro-benchmark
+    """This round's profile directories (profiles/<ROUND>*), oldest first by their stamp: micro-benchmark
     ceilings are quoted only when they were measured beside this round's kernels."""
     if not os.path.isdir(profiles_dir):
         return []
-    return [d for d in sorted(os.listdir(profiles_dir)) if d.startswith(ROUND)]
+
+    def utc(d):  # stamped directories in stamp order (tools/stamp.py), unstamped ones first
+        f = os.path.join(profiles_dir, d, "stamp.json")
+        try:
+            return json.load(open(f)).get("utc", "") if os.path.exists(f) else ""
+        except Exception:
+            return ""
+    return sorted((d for d in os.listdir(profiles_dir) if d.startswith(ROUND)), key=lambda d: (utc(d), d))
 
 
 def write_ceilings(profiles_dir=os.path.join(ROOT, "profiles")):
@@ -194,11 +221,12 @@ def beyond_cache(steps=20):
         ctx.close()
 
 
-def ifft_measure(ctx, reps, csv_name, pmc_config):
+def ifft_measure(ctx, reps, record_config):
     """The operator IFFT (ocean_ifft2d over the 4 planes, IFFT.InverseFastFourierTransform x 4) of a
     context: wall time (no events) and kernel time (HIP events attached to every launch) per call,
     algorithmic bytes 32 B per texel per plane (two passes x read + write), the symbols of the row
-    and column kernels that ran, and the committed rocprofv3 / PMC records of exactly those symbols.
+    and column kernels that ran, and the committed rocprofv3 / PMC records of exactly those symbols
+    (find_record: the record of `record_config` stamped with this library).
     Every call transforms freshly evolved planes (ocean_evolve before it): the unnormalised inverse
     transform grows the data by ~N per call, to inf / NaN within a dozen calls, and constant or zero
     data runs at a higher clock (MI355X_MICROARCH.md).  Wall = (evolve + operator) - (evolve alone)."""
@@ -230,21 +258,20 @@ def ifft_measure(ctx, reps, csv_name, pmc_config):
     fft_bytes = 32 * n * n * 4 * units
     stage_us = 1e6 * ((s1 - s0) - (s2 - s1)) / reps
     kern_us = 1e3 * (r_ms + c_ms) / reps
-    rp = {k: rocprof_kernel_us(csv_name, v) for k, v in syms.items()}
-    rocprof = None
-    if rp["rows"] and rp["cols"]:
-        # launches per call: rows and columns may run per unit chunk (ocean_abi.cpp)
-        lr, lc = r_n / reps, c_n / reps
-        rus = rp["rows"][0] * lr + rp["cols"][0] * lc
-        rocprof = {"source": rp["cols"][1], "rows_us": round(rp["rows"][0], 2), "cols_us": round(rp["cols"][0], 2),
+    rp = {k: find_record(record_config, v) for k, v in syms.items()} if record_config else {}
+    rocprof = traffic = None
+    lr, lc = r_n / reps, c_n / reps  # launches per call: rows and columns may run per unit chunk (ocean_abi.cpp)
+    if rp.get("rows") and rp.get("cols"):
+        rus = rp["rows"]["avg_us"] * lr + rp["cols"]["avg_us"] * lc
+        rocprof = {"source": rp["cols"]["dir"], "record_match": rp["cols"]["match"], "utc": rp["cols"]["utc"],
+                   "rows_us": round(rp["rows"]["avg_us"], 2), "cols_us": round(rp["cols"]["avg_us"], 2),
                    "launches_per_call": [lr, lc], "achieved_GBs": round(fft_bytes / (rus * 1e-6) / 1e9, 1),
                    "frac": round(fft_bytes / (rus * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
-    traffic = None
-    if pmc_config:
-        tr = {k: pmc_traffic(v, pmc_config) for k, v in syms.items()}
-        if tr["rows"] and tr["cols"]:
-            traffic = {"rows_bytes_per_launch": tr["rows"][0], "cols_bytes_per_launch": tr["cols"][0],
-                       "source": f"profiles/{tr['cols'][1]}/pmc_summary.json"}
+        tr, tc = rp["rows"]["traffic_bytes_per_launch"], rp["cols"]["traffic_bytes_per_launch"]
+        if tr and tc:
+            traffic = {"rows_bytes_per_launch": tr, "cols_bytes_per_launch": tc,
+                       "bytes_per_call": int(tr * lr + tc * lc), "algorithmic_bytes_per_call": fft_bytes,
+                       "source": rp["cols"]["dir"]}
     return {"bytes": fft_bytes, "us_per_stage_wall": round(stage_us, 2), "us_per_stage_kernels": round(kern_us, 2),
             "row_launches": r_n // reps, "col_launches": c_n // reps,
             "rows_us": round(1e3 * r_ms / reps, 2), "cols_us": round(1e3 * c_ms / reps, 2),
@@ -265,12 +292,63 @@ def ifft_beyond_cache(reps=50):
         ctx.set_params(SCENE_PARAMS, SCENE_CASCADES)
         ctx.generate_noise_device(20251121)
         ctx.init_spectrum()
-        r = ifft_measure(ctx, reps, "ifft_bc_kernel_stats.csv", "ifft_bc")
+        r = ifft_measure(ctx, reps, "ifft_bc")
         r["workload"] = "4 tiles x 4 cascades x 1024^2, 4 planes: 512 MiB of planes (2x the Infinity Cache)"
         r["data"] = "freshly evolved planes before every call (frame data)"
         return r
     finally:
         ctx.close()
+
+
+def update_loop(steps=200, warmup=20):
+    """The reference's per-frame loop at cfg3, as a Unity host over this library runs it
+    (WaterBody.Update, WaterBody.cs:284-297): CalculateWavesTexturesAtTime with the mip chains of DERIV
+    and TURB regenerated every frame (GenerateMips, :191-192; OCEAN_F_MIPS), then one asynchronous
+    readback of displacement slice 0 per frame (AsyncGPUReadback.Request, :288) into the facade's
+    pinned ring, polled, and copied out when it lands (request.GetData<Color>().ToArray(), :295) --
+    ocean_hip.WaterBody.Update.  Reported beside `value` (the device frame without mips):
+    frames/s of that loop, its PCIe bytes per frame, the frame with mips alone, and the mip kernels' time
+    per frame from HIP events."""
+    wb = oh.scene_water_body(n=1024, n_cascades=4, seed=20251121).Awake()
+    ctx = wb.ctx
+    try:
+        for f in range(warmup):
+            ctx.step(f / 60.0)
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        for f in range(steps):
+            ctx.step((warmup + f) / 60.0)
+        ctx.synchronize()
+        step_s = (time.perf_counter() - t0) / steps
+        ctx.set_kernel_timing(True)
+        ctx.kernel_stats(0), ctx.kernel_stats(1), ctx.kernel_stats(2)
+        for f in range(steps):
+            ctx.step((warmup + f) / 60.0)
+        ka, _ = ctx.kernel_stats(0)
+        kb, _ = ctx.kernel_stats(1)
+        km, nm = ctx.kernel_stats(2)
+        ctx.set_kernel_timing(False)
+        mips_sym = ctx.kernel_name(2)
+        for f in range(warmup):
+            wb.Update(f / 60.0)
+        wb.WaitForReadback()
+        t0 = time.perf_counter()
+        for f in range(steps):
+            wb.Update((warmup + f) / 60.0)
+        wb.WaitForReadback()  # every requested readback has landed inside the timed region
+        loop_s = (time.perf_counter() - t0) / steps
+        slice_bytes = 1024 * 1024 * 16
+        return {"workload": "cfg3 (4 x 1024^2) frame + GenerateMips of DERIV and TURB + AsyncGPUReadback of "
+                            "DISP slice 0 every frame, ocean_hip.WaterBody.Update (WaterBody.cs:284-297)",
+                "frames_per_s": round(1.0 / loop_s, 2), "ms_per_frame": round(1e3 * loop_s, 4),
+                "pcie_bytes_per_frame": slice_bytes, "pcie_GBs": round(slice_bytes / loop_s / 1e9, 2),
+                "readback_ring_slots": wb.MAX_READBACKS_IN_FLIGHT,
+                "step_with_mips": {"frames_per_s": round(1.0 / step_s, 2), "ms_per_frame": round(1e3 * step_s, 4),
+                                   "kernel_us": {"pass_a": round(1e3 * ka / steps, 2), "pass_b": round(1e3 * kb / steps, 2),
+                                                 "mips": round(1e3 * km / steps, 2)},
+                                   "mip_launches_per_frame": nm / steps, "mips_symbol_last": mips_sym}}
+    finally:
+        wb.OnDisable()
 
 
 def cpu_baseline(cfg, frames=3):
@@ -331,6 +409,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ifft-stage", action="store_true")
     ap.add_argument("--no-beyond-cache", action="store_true")
+    ap.add_argument("--no-update-loop", action="store_true")
     ap.add_argument("--no-interleave", action="store_true",
                     help="cfg5 past one GPU per cascade: contiguous column bands instead of even / odd columns")
     args = ap.parse_args()
@@ -451,8 +530,10 @@ def main():
     # chunk_units); bytes per step / time per step = bytes per launch / time per launch
     a_us = 1e3 * ka_ms / args.steps
     b_us = 1e3 * kb_ms / args.steps
-    launches_per_step = max(kb_n, 1) / args.steps
     dom, dom_us = ("pass_b", b_us) if b_us >= a_us else ("pass_a", a_us)
+    # launches of the dominant kind per step (each pass runs once per unit chunk; at N >= 2048 the
+    # column kind is C1 + C2 per (unit, band), so per-launch figures there mix the two kernels)
+    launches_per_step = max(kb_n if dom == "pass_b" else ka_n, 1) / args.steps
     if args.unfused:
         dom = "ifft_cols" if dom == "pass_b" else "ifft_rows"
     dom_bytes = B["pass_b" if dom in ("pass_b", "ifft_cols") else "pass_a"]
@@ -470,15 +551,16 @@ def main():
         # operator-level stage (IFFT.InverseFastFourierTransform x 4 planes), unfused kernels, on the
         # frame's own planes (ocean_evolve before every call): the fused frame never writes them, and
         # zero-filled planes run at a higher clock (MI355X_MICROARCH.md) -- rounds 1-2 timed zeros
-        # PMC records of the operator's kernels: cfg3's (tools/profile.sh) and the 4 x 4096^2 operator's
-        # (profiles/r03zzz_op4k, config "op4k": the same launches per unit-plane chunk as cfg5's)
-        ifft_stage = ifft_measure(ctx, max(20, args.steps // 5), "ifft_kernel_stats.csv",
-                                  {"cfg3": "cfg3", "cfg5": "op4k"}.get(args.config))
+        # rocprofv3 + PMC records of the operator's kernels (tools/profile.sh): config "ifft" for cfg3's
+        # 4 x 1024^2 x 4 planes, "op4k" for the 4 x 4096^2 operator (the same launches per unit-plane
+        # chunk as cfg5's)
+        ifft_stage = ifft_measure(ctx, max(20, args.steps // 5), {"cfg3": "ifft", "cfg5": "op4k"}.get(args.config))
         ifft_stage["data"] = "freshly evolved planes before every call (frame data)"
         if rank == 0 and world == 1 and args.config == "cfg3" and not args.no_beyond_cache:
             ifft_stage["beyond_cache"] = ifft_beyond_cache()
 
-    traffic = pmc_traffic(dom_sym, args.config) if not args.unfused else None
+    record = find_record(args.config, dom_sym) if not args.unfused else None
+    traffic = record["traffic_bytes_per_launch"] if record else None
     # the dominant kernel's store stream against the chip's measured store ceiling: pass B writes the
     # textures (16 B DISP [+ 32 B DERIV, TURB] [+ 16 B NORMAL]) and the 4-B foam state per texel
     writes = None
@@ -501,6 +583,9 @@ def main():
                  "note": "the frame's re-read set (h0k + intermediate + foam state) fits the Infinity Cache, "
                          "so part of `achieved` is cache bandwidth; beyond_cache is the HBM-bound figure",
                  "beyond_cache": beyond_cache()}
+    update = None
+    if rank == 0 and world == 1 and args.config == "cfg3" and not args.unfused and not args.no_update_loop:
+        update = update_loop(max(50, args.steps // 2), args.warmup)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg)
@@ -532,9 +617,15 @@ def main():
                                       f"over {world} GPU(s), no collective"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic[0] if traffic else None,
-                         "traffic_source": f"profiles/{traffic[1]}/pmc_summary.json" if traffic else None,
+                         "traffic": traffic,  # HBM bytes per launch (PMC), like `achieved`
+                         "traffic_per_step": int(traffic * launches_per_step) if traffic else None,
+                         "traffic_source": record["dir"] if record else None,
+                         "record": ({k: record[k] for k in ("match", "utc", "git_head", "avg_us")}
+                                    if record else None),
+                         "rocprof_frac": (round(dom_bytes / launches_per_step / (record["avg_us"] * 1e-6) / 1e9
+                                                / HBM_PEAK_GBS, 4) if record else None),
                          "kernel_symbol": dom_sym,
+                         "algorithmic_bytes_per_launch": int(dom_bytes / launches_per_step),
                          "algorithmic_bytes_per_step": dom_bytes, "kernel_us_per_step": round(dom_us, 3),
                          "launches_per_step": round(launches_per_step, 2),
                          "writes": writes, "memory_shape": shape},
@@ -546,6 +637,7 @@ def main():
                       "ms_per_step_with_kernel_events": round(1e3 * elapsed_ev / args.steps, 5)},
             "ifft_stage": ifft_stage,
             "cache": cache,
+            "update_loop": update,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

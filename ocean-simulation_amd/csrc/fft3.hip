@@ -22,8 +22,6 @@
 //
 // Bytes per texel-cascade (P = 4): pass A 16 (h0; 8 for A4) + 32 (planes);
 // pass B 32 (planes) + 4 + 4 (foam) + 48 (DISP, DERIV, TURB) = 88.
-#include <cstdlib>
-
 #include <type_traits>
 
 #include "fft_engine.h"
@@ -37,12 +35,12 @@ constexpr int pa3_rows(int N, int RS = 2) { return N >= 1024 * RS ? 1 : 1024 * R
 // RS: row-sets per workgroup (RB = pa3_rows(N, RS) rows); PF: prefetch the
 // next item's h0 before this item's transform (its loads are then ahead of
 // this item's stores in the in-order vmcnt queue, so waiting for them never
-// waits for the stores); NOSTORE: timing experiment only (no output); BAND: a
+// waits for the stores); BAND: a
 // column band narrower than N (stores outside it skipped; a separate instance so
 // that the whole-band frame pays no per-store test).  EPF (without PF): the next item's h0 is
 // loaded into h as soon as the evolve has read it, in flight across the stages (+16-19 VGPRs:
 // N = 4096 only, where the workgroup's occupancy does not change); else after the stages.
-template <int N, int P, int RS, bool PF, bool NOSTORE = false, bool BAND = false, int WT = 0, bool EPF = false>
+template <int N, int P, int RS, bool PF, bool BAND = false, int WT = 0, bool EPF = false>
 __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems) void k_pass_a3(DevView v, float time, int total_rows) {
     constexpr int RB = pa3_rows(N, RS);
     constexpr int FIRST = 16 / P;
@@ -101,10 +99,6 @@ __global__ __launch_bounds__(pa3_rows(N, RS) * P * N / kElems) void k_pass_a3(De
         }
         // outputs: sequence b = p*RB + rr', element x -> tplane[p][u'][x/W][y'][x%W]
         auto emit = [&](int m, int q, float2 val) {
-            if constexpr (NOSTORE) {
-                asm volatile("" ::"v"(val.x), "v"(val.y));
-                return;
-            }
             int b, jj;
             E::template bj<E::RL>((int)threadIdx.x + m * T, b, jj);
             const int p = b / RB, r2 = b % RB;
@@ -414,16 +408,15 @@ __global__ __launch_bounds__(2 * W * N / 8) void k_pass_b8(DevView v, int items)
 // jm = (NJ - j) % NJ of row y2, whose texels are the mirrors of its own: two
 // radix-4 butterflies x 4 planes = 32 values per lane (Engine EL = 32).
 //
-// PH: planes per LDS pass.  PH = 2 (default) holds 4 of the 8 sequences in LDS (planes
-// p0, p0 + 1 of both rows) and runs the stages twice per item: 43.5 KiB of LDS instead of
-// 78 KiB, so 3 workgroups share a CU instead of 2 and the per-workgroup latency chain
-// (evolve -> LDS stages -> stores) overlaps better: 38.6 -> 33.0 us at cfg3.
+// PH = 2 planes per LDS pass: 4 of the 8 sequences in LDS (planes p0, p0 + 1 of both rows),
+// the stages run twice per item: 43.5 KiB of LDS instead of 78 KiB, so 3 workgroups share a
+// CU instead of 2 and the per-workgroup latency chain (evolve -> LDS stages -> stores)
+// overlaps better: 38.6 -> 33.0 us at cfg3.
 //
-// P = 2 (displacement-only frames, N = 256 and 512): both planes in one LDS pass.
-template <int N, bool NOSTORE = false, bool BAND = false, int PH = 2, int WT = 0, int P = 4>
+// P = 2 (displacement-only frames, N = 256): both planes in one LDS pass.
+template <int N, bool BAND = false, int WT = 0, int P = 4>
 __global__ __launch_bounds__(N / 4) void k_pass_a4(DevView v, float time, int items_per_unit, int items) {
-    constexpr int R0 = 4, RB = 2, EL = 2 * P * R0;
-    static_assert(PH == 2 || PH == 4, "stages need 16 values per lane");
+    constexpr int R0 = 4, RB = 2, EL = 2 * P * R0, PH = 2;
     using TW = StageTw<N, R0>;
     using E = Engine<N, RB * PH, false, true, R0, TW, EL * PH / P>;
     constexpr int T = E::THREADS;
@@ -537,10 +530,6 @@ __global__ __launch_bounds__(N / 4) void k_pass_a4(DevView v, float time, int it
             }
             __syncthreads();
             auto emit = [&](int m, int q, float2 val) {
-                if constexpr (NOSTORE) {
-                    asm volatile("" ::"v"(val.x), "v"(val.y));
-                    return;
-                }
                 int b, jj;
                 E::template bj<E::RL>((int)threadIdx.x + m * T, b, jj);
                 if (BAND && (unsigned)(jj + q * NSL - v.x0) >= (unsigned)v.nx) return;  // outside the column band
@@ -712,50 +701,37 @@ __global__ __launch_bounds__(N / 2) void k_pass_a8(DevView v, float time, int it
     }
 }
 
-int env_int(const char* name, int dflt) {
-    const char* e = std::getenv(name);
-    return e ? std::atoi(e) : dflt;
-}
-
 template <class K>
 int grid3(K kernel, int threads, int items) {
     const int g = device_cus() * resident_per_cu((const void*)kernel, threads);
     return items < g ? items : g;
 }
 
-template <int N, int P, int RS, bool PF, bool NOSTORE = false, bool BAND = false, int WT = 0>
+// EPF at N = 4096: the next row's h0 in flight across the stages (641 against 658 us)
+template <int N, int P, int RS, bool PF, bool BAND = false, int WT = 0>
 hipError_t go_a3k(const DevView& v, float t, hipStream_t s) {
     if constexpr (WT == 0 && N >= 128 && N <= 1024) {
-        if (v.tile_w != inter_w(N)) return go_a3k<N, P, RS, PF, NOSTORE, BAND, 4>(v, t, s);
+        if (v.tile_w != inter_w(N)) return go_a3k<N, P, RS, PF, BAND, 4>(v, t, s);
     }
-    if constexpr (!BAND && !NOSTORE) {
-        if (v.nx != N) return go_a3k<N, P, RS, PF, false, true, WT>(v, t, s);
+    if constexpr (!BAND) {
+        if (v.nx != N) return go_a3k<N, P, RS, PF, true, WT>(v, t, s);
     }
     constexpr int RB = pa3_rows(N, RS);
     constexpr int T = RB * P * N / kElems;
     const int total = v.units * N;
     const int items = (total + RB - 1) / RB;
     constexpr bool EPF = (N == 4096);
-    static const int epf = env_int("OCEAN_A3_EPF", 1);  // 0: N = 4096 loads the next row after the stages (A/B)
-    if (EPF && !epf) {
-        const int g = grid3(k_pass_a3<N, P, RS, PF, NOSTORE, BAND, WT, false>, T, items);
-        launch((k_pass_a3<N, P, RS, PF, NOSTORE, BAND, WT, false>), dim3(g), dim3(T), 0, s, v, t, total);
-        return hipGetLastError();
-    }
-    const int g = grid3(k_pass_a3<N, P, RS, PF, NOSTORE, BAND, WT, EPF>, T, items);
-    launch((k_pass_a3<N, P, RS, PF, NOSTORE, BAND, WT, EPF>), dim3(g), dim3(T), 0, s, v, t, total);
+    const int g = grid3(k_pass_a3<N, P, RS, PF, BAND, WT, EPF>, T, items);
+    launch((k_pass_a3<N, P, RS, PF, BAND, WT, EPF>), dim3(g), dim3(T), 0, s, v, t, total);
     return hipGetLastError();
 }
 
 // N = 1024, 4 planes: 2 rows per workgroup (512 lanes) with the next item's h0
-// prefetched; other sizes: pa3_rows(N, 1) rows.  OCEAN_A3_VARIANT=11 is a timing
-// build without the intermediate stores (pass A).
+// prefetched; other sizes: pa3_rows(N, 1) rows.
 template <int N, int P>
 hipError_t go_a3(const DevView& v, float t, hipStream_t s) {
-    static const bool nostore = env_int("OCEAN_A3_VARIANT", 0) == 11;
-    if constexpr (N == 1024 && P == 4)
-        return nostore ? go_a3k<N, P, 2, true, true>(v, t, s) : go_a3k<N, P, 2, true>(v, t, s);
-    return nostore ? go_a3k<N, P, 1, false, true>(v, t, s) : go_a3k<N, P, 1, false>(v, t, s);
+    if constexpr (N == 1024 && P == 4) return go_a3k<N, P, 2, true>(v, t, s);
+    return go_a3k<N, P, 1, false>(v, t, s);
 }
 
 template <int N, int P, int PFD, int WT = 0>
@@ -794,34 +770,32 @@ hipError_t go_b8(const DevView& v, hipStream_t s) {
 
 // Two planes in flight at N = 1024 (one workgroup per CU, registers to spare).  Displacement-only
 // frames (P = 2) on narrow tiles run both planes side by side: pass B8 at N = 512 (8 values per
-// lane; OCEAN_B8=0: k_pass_b2d), k_pass_b2d at N = 128..256 (OCEAN_B2D=0: one after the other).
+// lane), k_pass_b2d at N = 128..256.
 template <int N, int P>
 hipError_t go_b3(const DevView& v, hipStream_t s) {
     if constexpr (P == 2 && N == 512) {
-        static const int b8 = env_int("OCEAN_B8", 1);  // 0: pass B2D (16 values per lane) on narrow tiles
-        if (b8 && v.tile_w == 4) return go_b8<N>(v, s);
+        if (v.tile_w == 4) return go_b8<N>(v, s);
     }
-    if constexpr (P == 2 && N >= 128 && N <= 512) {
-        static const int b2d = env_int("OCEAN_B2D", 1);
-        if (b2d && v.tile_w == 4) return go_b2d<N>(v, s);
+    if constexpr (P == 2 && N >= 128 && N <= 256) {
+        if (v.tile_w == 4) return go_b2d<N>(v, s);
     }
     if constexpr (N == 1024) return go_b3k<N, P, 2>(v, s);
     return go_b3k<N, P, 1>(v, s);
 }
 
-template <int N, bool NOSTORE = false, bool BAND = false, int PH = 2, int WT = 0, int P = 4>
+template <int N, bool BAND = false, int WT = 0, int P = 4>
 hipError_t go_a4(const DevView& v, float t, hipStream_t s) {
     if constexpr (WT == 0) {
-        if (v.tile_w != inter_w(N)) return go_a4<N, NOSTORE, BAND, PH, 4, P>(v, t, s);
+        if (v.tile_w != inter_w(N)) return go_a4<N, BAND, 4, P>(v, t, s);
     }
-    if constexpr (!BAND && !NOSTORE) {
-        if (v.nx != N) return go_a4<N, false, true, PH, WT, P>(v, t, s);
+    if constexpr (!BAND) {
+        if (v.nx != N) return go_a4<N, true, WT, P>(v, t, s);
     }
     constexpr int T = N / 4;
     const int ipu = N / 2;
     const int items = v.units * ipu;
-    const int g = grid3(k_pass_a4<N, NOSTORE, BAND, PH, WT, P>, T, items);
-    launch((k_pass_a4<N, NOSTORE, BAND, PH, WT, P>), dim3(g), dim3(T), 0, s, v, t, ipu, items);
+    const int g = grid3(k_pass_a4<N, BAND, WT, P>, T, items);
+    launch((k_pass_a4<N, BAND, WT, P>), dim3(g), dim3(T), 0, s, v, t, ipu, items);
     return hipGetLastError();
 }
 
@@ -837,29 +811,21 @@ hipError_t go_a8(const DevView& v, float t, hipStream_t s) {
 
 }  // namespace
 
+// N = 512 / 1024 with four planes; N = 256 / 512 displacement-only (two planes)
 bool pass_a4_supported(int n, int planes) {
-    // bit 0: N = 1024, bit 1: N = 512 (4 planes); bit 2: N = 256 / 512 (2 planes)
-    static const int on = env_int("OCEAN_A4_SIZES", 7);
-    if (planes == 2) return (on & 4) && (n == 256 || n == 512);
-    return planes == 4 && ((n == 1024 && (on & 1)) || (n == 512 && (on & 2)));
+    if (planes == 2) return n == 256 || n == 512;
+    return planes == 4 && (n == 512 || n == 1024);
 }
 
+// P = 2 at N = 512: pass A8 (256 lanes, 8 values each; 6.64 against 7.47 us for pass A4's two-plane
+// layout at cfg2)
 hipError_t launch_pass_a_v4(const DevView& v, float t, hipStream_t s) {
     if (!pass_a4_supported(v.n, v.planes) || !v.h0k) return hipErrorInvalidValue;
-    static const int nostore = env_int("OCEAN_A4_NOSTORE", 0);
-    static const int whole = env_int("OCEAN_A4_WHOLE", 0);  // 1: all 4 planes in one LDS pass (A/B)
     if (v.planes == 2) {
-        if (v.n == 256) return go_a4<256, false, false, 2, 0, 2>(v, t, s);
-        static const int a8 = env_int("OCEAN_A8", 1);  // 0: pass A4's 4-values-per-texel-pair layout at N = 512
-        if (a8) return v.tile_w == inter_w(512) ? go_a8<512, 0>(v, t, s) : go_a8<512, 4>(v, t, s);
-        return go_a4<512, false, false, 2, 0, 2>(v, t, s);
+        if (v.n == 256) return go_a4<256, false, 0, 2>(v, t, s);
+        return v.tile_w == inter_w(512) ? go_a8<512, 0>(v, t, s) : go_a8<512, 4>(v, t, s);
     }
-    if (v.n == 512) {
-        if (whole) return go_a4<512, false, false, 4>(v, t, s);
-        return nostore ? go_a4<512, true>(v, t, s) : go_a4<512>(v, t, s);
-    }
-    if (whole) return go_a4<1024, false, false, 4>(v, t, s);
-    return nostore ? go_a4<1024, true>(v, t, s) : go_a4<1024>(v, t, s);
+    return v.n == 512 ? go_a4<512>(v, t, s) : go_a4<1024>(v, t, s);
 }
 
 hipError_t launch_pass_a_v3(const DevView& v, float t, hipStream_t s) {

@@ -8,10 +8,6 @@
 #include "fft_core.h"
 #include "ocean_internal.h"
 
-#ifndef OCEAN_NO_WAVE_PRIVATE
-#define OCEAN_NO_WAVE_PRIVATE 0  // 1: workgroup barriers between all stages (A/B builds)
-#endif
-
 namespace ocean {
 namespace {
 using namespace fftcore;
@@ -278,7 +274,7 @@ struct Engine {
     // every such stage) and the stages need no workgroup barrier -- LDS operations of
     // one wave execute in order; a compiler fence keeps them in program order.
     static constexpr bool wave_private(int st) {
-        if (SEQ_FAST || OCEAN_NO_WAVE_PRIVATE) return false;
+        if (SEQ_FAST) return false;
         for (int s = st; s < S; ++s)
             if (N / radix_of(N, s, FIRST) != 64) return false;
         return st < S;
@@ -395,11 +391,7 @@ struct ColTile {
     static constexpr int W = WW;
     static constexpr int tiles = N / W;
     using TW = StageTwLds<N>;
-#ifdef OCEAN_NO_COLPAD  // A/B builds only
-    using E = Engine<N, W, true, false, 16, TW>;
-#else
     using E = Engine<N, W, true, Engine<N, W, true, false>::seq_pad_ok(), 16, TW>;
-#endif
     static constexpr int T = E::THREADS;
     static constexpr int R0 = E::R0, RL = E::RL;
     static __device__ __forceinline__ int lane_b() { return (int)threadIdx.x % W; }

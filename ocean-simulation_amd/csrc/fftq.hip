@@ -19,44 +19,8 @@
 // The planes Q1..Q3 (24 B / texel instead of 32) plus the per-unit side arrays d0 and srow are the
 // whole intermediate; pass B forms R[Q4] from R[Q1] on load.  The outputs equal the four-plane
 // frame's in real arithmetic, Nyquist lines included; in fp32 they differ by rounding only.
-#include <cstdlib>
 #include "fft_engine.h"
 #include "spectrum_math.h"
-
-#ifndef OCEAN_AQ_WPEU
-#define OCEAN_AQ_WPEU 0  // waves per SIMD pass AQ is compiled for (0: the compiler's choice; A/B builds)
-#endif
-#ifndef OCEAN_AQ_CTW
-#define OCEAN_AQ_CTW 0  // 1: compact LDS twiddle tables in pass AQ (37.4 instead of 43.5 KiB; A/B builds)
-#endif
-#ifndef OCEAN_AQ_RCP
-#define OCEAN_AQ_RCP 1  // pass AQ takes 1/|k| from the hardware reciprocal: cfg3 pass A 29.8 -> 28.6-29.3 us
-#endif
-#ifndef OCEAN_AQ_SHARE
-#define OCEAN_AQ_SHARE 0  // 1: pass AQ also exchanges the in-row mirror texels' factors through LDS (A/B builds)
-#endif
-#ifndef OCEAN_AQ_WST
-#define OCEAN_AQ_WST 1  // pass AQ's intermediate stores: scalar unit base + 32-bit lane offsets (0: 64-bit addresses; A/B)
-#endif
-#ifndef AQ_SKIP
-#define AQ_SKIP 1  // pass AQ's idle pass-1 waves skip the stages (A/B builds)
-#endif
-#ifndef A3P_EARLY_PF
-#define A3P_EARLY_PF 1
-#endif
-#ifndef OCEAN_A3P_WPEU
-#define OCEAN_A3P_WPEU 0  // waves per SIMD pass A3P is compiled for (0: the compiler's choice; A/B builds)
-#endif
-#if OCEAN_A3P_WPEU
-#define A3P_WPEU __attribute__((amdgpu_waves_per_eu(OCEAN_A3P_WPEU)))
-#else
-#define A3P_WPEU
-#endif
-#if OCEAN_AQ_WPEU
-#define AQ_WPEU __attribute__((amdgpu_waves_per_eu(OCEAN_AQ_WPEU)))
-#else
-#define AQ_WPEU
-#endif
 
 namespace ocean {
 namespace {
@@ -136,12 +100,15 @@ __device__ __forceinline__ float2* q_side(const DevView& v, int u) { return v.qs
 // first and are not stored, except that item 0 carries srow in its second Q3 slot.  Lane j
 // evolves texels x = j + r N/4 of row y1 with their mirrors (N - x) % N in row y2 and holds
 // stage-0 butterfly j of row y1 and jm = (N/4 - j) % (N/4) of row y2.  LDS pass 0: Q1, Q2 of both
-// rows; pass 1: Q3 of both rows (two of its four sequence slots idle).
-template <int N, bool BAND = false, int WT = 0>
-__global__ __launch_bounds__(N / 4) AQ_WPEU void k_pass_aq(DevView v, float time, int items) {
+// rows; pass 1: Q3 of both rows (two of its four sequence slots idle, their butterflies skipped).
+// OFF32: the intermediate stores take a scalar unit base and a 32-bit lane offset (plane, row, tile,
+// column) instead of a 64-bit address (cfg3 pass A 29.15-29.40 -> 28.26-29.15 us); the host checks
+// that the chunk's three planes lie within 4 GiB of the base (go_aq), else the 64-bit form runs.
+template <int N, bool BAND = false, int WT = 0, bool OFF32 = true>
+__global__ __launch_bounds__(N / 4) void k_pass_aq(DevView v, float time, int items) {
     constexpr int R0 = 4, NJ = N / R0;
     constexpr int IPU = N / 2 + 1;  // items per unit
-    using TW = std::conditional_t<OCEAN_AQ_CTW, StageTwCompact<N, R0>, StageTw<N, R0>>;
+    using TW = StageTw<N, R0>;
     using E = Engine<N, 4, false, true, R0, TW, kElems>;
     constexpr int T = E::THREADS;
     static_assert(T == NJ && E::R0 == R0, "lane j <-> stage-0 butterfly j");
@@ -155,9 +122,6 @@ __global__ __launch_bounds__(N / 4) AQ_WPEU void k_pass_aq(DevView v, float time
     const float2* tws = TW::table(twl, v.tw);
     __shared__ WaveBand band[kMaxCascades];
     if ((int)threadIdx.x < v.C) band[threadIdx.x] = wave_band(v.casc + threadIdx.x * 5);
-#if OCEAN_AQ_SHARE
-    __shared__ float4 xch[2 * NJ];  // (e.x, e.y, 1/|k|, -) of texel j + r NJ of row y1 at [r][j], r < 2
-#endif
     const int j = (int)threadIdx.x;
     const int jm = (NJ - j) & (NJ - 1);
     const bool j0 = (j == 0);
@@ -197,40 +161,17 @@ __global__ __launch_bounds__(N / 4) AQ_WPEU void k_pass_aq(DevView v, float time
         rows_of(it, u, y1, y2);
         const WaveBand wb = band[(u + v.c0) % v.C];
         const bool self = (y1 == y2);
-#if OCEAN_AQ_WST
         const Win wunit = make_win(v.tplane + (size_t)u * TILES * N * W, 0);
-#endif
-#if OCEAN_AQ_SHARE
-        float4 own[2];
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            own[r] = mirror_factors<N>(j + r * NJ, y1, wb, v.gravity, time);
-            xch[r * NJ + j] = own[r];
-        }
-        __syncthreads();
-#endif
         // after stage 0: g = (Q1 y1, Q1 y2, Q2 y1, Q2 y2, Q3 y1, Q3 y2 | row 0: srow's input)
         float2 g[6][R0];
         {
             float2 mir[3][R0];
 #pragma unroll
             for (int r = 0; r < R0; ++r) {
-#if OCEAN_AQ_SHARE
-                // texels x and N - x of row y1 share the factors: r < 2 evaluated here, r >= 2 exchanged
-                const int rp = j0 ? R0 - r : R0 - 1 - r;
-                const float4 f = (r < 2) ? own[r] : (rp < 2) ? xch[(rp & 1) * NJ + jm]
-                                                             : mirror_factors<N>(j + r * NJ, y1, wb, v.gravity, time);
-                const float4 wd = make_float4((float)(j + r * NJ - N / 2) * wb.dk, f.z, (float)(y1 - N / 2) * wb.dk, 0.0f);
-                const float2 h = evolve_h(make_float4(A[r].x, A[r].y, B[r].x, -B[r].y), Phase{f.x, f.y});
-#elif OCEAN_AQ_RCP
                 // hardware reciprocal for 1/|k| (mirror_factors); omega and the phase as wave_data's
                 const float4 f = mirror_factors<N>(j + r * NJ, y1, wb, v.gravity, time);
                 const float4 wd = make_float4((float)(j + r * NJ - N / 2) * wb.dk, f.z, (float)(y1 - N / 2) * wb.dk, 0.0f);
                 const float2 h = evolve_h(make_float4(A[r].x, A[r].y, B[r].x, -B[r].y), Phase{f.x, f.y});
-#else
-                const float4 wd = wave_data(j + r * NJ, y1, N, wb, v.gravity);
-                const float2 h = evolve_h(make_float4(A[r].x, A[r].y, B[r].x, -B[r].y), evolve_phase(wd.w, time));
-#endif
                 QTex qa, qb;
                 if (y1 != 0 && !(r == 0 && j0)) {
                     q_fast(h, wd, qa, qb);
@@ -284,21 +225,21 @@ __global__ __launch_bounds__(N / 4) AQ_WPEU void k_pass_aq(DevView v, float time
                     return;
                 }
                 if (BAND && (unsigned)(x - v.x0) >= (unsigned)v.nx) return;  // outside the column band
-#if OCEAN_AQ_WST
-                // scalar unit base + a 32-bit lane offset (plane, row, tile, column; < 4 GiB, host-checked):
-                // one 32-bit add per store instead of a 64-bit address
-                const unsigned off = (unsigned)p * (unsigned)(v.inter_stride * 8) +
-                                     (unsigned)((((s ? y2 : y1) * W) + (jj / W) * N * W + (jj % W)) * 8);
-                gstore2(val, wunit, (int)off, q * (NSL / W) * N * W * 8);
-#else
-                float2* dst = v.tplane + (size_t)p * v.inter_stride + ((size_t)u * TILES * N + (s ? y2 : y1)) * W +
-                              (size_t)(jj / W) * N * W + (jj % W);
-                dst[(size_t)q * (NSL / W) * N * W] = val;
-#endif
+                if constexpr (OFF32) {
+                    // scalar unit base + a 32-bit lane offset (plane, row, tile, column; < 4 GiB, go_aq):
+                    // one 32-bit add per store instead of a 64-bit address
+                    const unsigned off = (unsigned)p * (unsigned)(v.inter_stride * 8) +
+                                         (unsigned)((((s ? y2 : y1) * W) + (jj / W) * N * W + (jj % W)) * 8);
+                    *(float2*)(wunit.p + (store_off_t)(off + (unsigned)(q * (NSL / W) * N * W * 8))) = val;
+                } else {
+                    float2* dst = v.tplane + (size_t)p * v.inter_stride +
+                                  ((size_t)u * TILES * N + (s ? y2 : y1)) * W + (size_t)(jj / W) * N * W + (jj % W);
+                    dst[(size_t)q * (NSL / W) * N * W] = val;
+                }
             };
             // pass 1: sequence slots 2, 3 idle, their butterflies skipped (at N = 1024 the stages are
             // wave-private, wave w = sequence w: waves 2, 3 skip them whole)
-            E::template stages_from<1>(lds, tws, emit, (AQ_SKIP && ps == 1) ? 2 : 4);
+            E::template stages_from<1>(lds, tws, emit, ps == 1 ? 2 : 4);
             __syncthreads();
         }
 #pragma unroll
@@ -310,25 +251,17 @@ __global__ __launch_bounds__(N / 4) AQ_WPEU void k_pass_aq(DevView v, float time
 }
 
 // Pass A3Q (N = 4096): the three-plane row pass in the shape of k_pass_a3 (fft3.hip):
-// one row per item, lane j holds texels j + r N/4 (r < 4) of four sequences, transformed
-// together: Q1, Q2, Q3 and, on row 0, srow's input (Q4 of row 0; the slot is idle on other
-// rows).  P(-k) is formed from the lane's own texel: h(-k) = conj h(k) bit for bit (h0.zw =
-// conj h0(-k) after ocean_init_spectrum), with the mirror's wave data (kx, kz negated except on
-// the Nyquist column / row).  16-wide tile-major intermediate as pass A3.
-// S3: the LDS stages skip the idle fourth sequence slot (its butterflies' lanes only join the
-// stage barriers); row 0 runs srow's input through them in a second pass (one row in N).
-// SLIM (N = 1024, A/B): compact twiddles and an LDS image of the three live sequence slots only
-// (S3: slot 3 is never touched; row 0's srow runs through slot 0), 28.6 instead of 43.5 KiB, so four
-// 256-lane workgroups share a CU where the VGPRs allow it.
-// SHARE: texels x and N - x of a row share omega, 1/|k| and the phase factor (mirror_factors): lane
-// j evaluates them for its texels r < 2 and reads r >= 2 from the mirror lane NJ - j (r' = 3 - r;
-// lane 0: r' = 4 - r, and x = N/2 itself) through LDS -- a separate 8 KiB buffer at N = 1024, the
-// (then idle) image at N = 4096 with one more barrier before stage 0.
-template <int N, bool BAND = false, bool S3 = true, bool EARLY_PF = true, bool SLIM = false, bool SHARE = false>
+// one row per item, lane j holds texels j + r N/4 (r < 4) of the sequences Q1, Q2, Q3 and, on row 0,
+// srow's input (Q4 of row 0).  P(-k) is formed from the lane's own texel: h(-k) = conj h(k) bit for
+// bit (h0.zw = conj h0(-k) after ocean_init_spectrum), with the mirror's wave data (kx, kz negated
+// except on the Nyquist column / row).  16-wide tile-major intermediate as pass A3.  The LDS stages
+// skip the idle fourth sequence slot (its butterflies' lanes only join the stage barriers); row 0 runs
+// srow's input through them in a second pass (one row in N).  The next row's h0 is loaded right after
+// the evolve has read the current row's, in flight across the row's stages (567 -> 517 us at cfg5).
+template <int N, bool BAND = false>
 __global__ __launch_bounds__(N / 4) void k_pass_a3q(DevView v, float time, int total_rows) {
     constexpr int FIRST = 4;
-    static_assert(!SLIM || S3, "the slim image holds the three live slots of the S3 schedule");
-    using TW = std::conditional_t<SLIM, StageTwCompact<N, FIRST>, StageTwLds<N, FIRST>>;
+    using TW = StageTwLds<N, FIRST>;
     using E = Engine<N, 4, false, true, FIRST, TW>;
     constexpr int T = E::THREADS;
     constexpr int R0 = E::R0;
@@ -337,12 +270,7 @@ __global__ __launch_bounds__(N / 4) void k_pass_a3q(DevView v, float time, int t
     constexpr int TILES = N / W;
     constexpr int NSL = N / E::RL;
     static_assert(T == NJ && R0 == 4, "lane j <-> stage-0 butterfly j of each sequence");
-    constexpr bool XSEP = SHARE && N <= 1024;  // exchange buffer of its own (else aliased on the image)
-    __shared__ __align__(16) float2 lds[SLIM ? E::LDS_ELEMS / 4 * 3 : E::LDS_ELEMS];
-    __shared__ float4 xsep[XSEP ? 2 * NJ : 1];
-    float4* xch = XSEP ? xsep : reinterpret_cast<float4*>(lds);
-    static_assert(XSEP || !SHARE || 2 * NJ * 16 <= (SLIM ? E::LDS_ELEMS / 4 * 3 : E::LDS_ELEMS) * 8, "xch fits");
-    const int jm = (NJ - (int)threadIdx.x) & (NJ - 1);
+    __shared__ __align__(16) float2 lds[E::LDS_ELEMS];
     __shared__ float2 twl[TW::kLdsEntries];
     TW::load(twl, v.tw, threadIdx.x, T);
     const float2* tws = TW::table(twl, v.tw);
@@ -365,32 +293,10 @@ __global__ __launch_bounds__(N / 4) void k_pass_a3q(DevView v, float time, int t
         const int u = item / N, y = item % N;
         const WaveBand wb = band[(u + v.c0) % v.C];
         float2 in[4 * R0];  // slot p * R0 + r: sequence p, stage-0 input r
-        float4 own[SHARE ? 2 : 1];
-        if constexpr (SHARE) {
-#pragma unroll
-            for (int r = 0; r < 2; ++r) {
-                own[r] = mirror_factors<N>(j + r * NJ, y, wb, v.gravity, time);
-                xch[r * NJ + j] = own[r];
-            }
-            __syncthreads();
-        }
 #pragma unroll
         for (int r = 0; r < R0; ++r) {
-            float4 wd;
-            Phase ph;
-            if constexpr (SHARE) {
-                float4 f;
-                const int rp = j0 ? 4 - r : 3 - r;  // the mirror's r' (< 2: exchanged; else evaluated here)
-                if (r < 2) f = own[r];
-                else f = (rp < 2) ? xch[(rp & 1) * NJ + jm] : mirror_factors<N>(j + r * NJ, y, wb, v.gravity, time);
-                wd = make_float4((float)(j + r * NJ - N / 2) * wb.dk, f.z, (float)(y - N / 2) * wb.dk, 0.0f);
-                ph.ex = f.x;
-                ph.ey = f.y;
-            } else {
-                wd = wave_data(j + r * NJ, y, N, wb, v.gravity);
-                ph = evolve_phase(wd.w, time);
-            }
-            const float2 hh = evolve_h(h[r], ph);
+            const float4 wd = wave_data(j + r * NJ, y, N, wb, v.gravity);
+            const float2 hh = evolve_h(h[r], evolve_phase(wd.w, time));
             QTex qa, qb;
             in[3 * R0 + r] = make_float2(0.0f, 0.0f);
             if (y != 0 && !(r == 0 && j0)) {
@@ -406,8 +312,7 @@ __global__ __launch_bounds__(N / 4) void k_pass_a3q(DevView v, float time, int t
             for (int p = 0; p < 3; ++p) in[p * R0 + r] = qa.q[p];
         }
         const int next = item + gridDim.x;
-        // the next row's h0 in flight across this row's stages (EARLY_PF; else after them)
-        if (EARLY_PF && next < total_rows) load(next, h);
+        if (next < total_rows) load(next, h);  // the next row's h0 in flight across this row's stages
         auto put = [&](int b, int jj, int q, float2 val) {
             const int x = jj + q * NSL;
             if (b == 3) {
@@ -415,179 +320,6 @@ __global__ __launch_bounds__(N / 4) void k_pass_a3q(DevView v, float time, int t
                 return;
             }
             if (BAND && (unsigned)(x - v.x0) >= (unsigned)v.nx) return;  // outside the column band
-            float2* rowp = v.tplane + (size_t)b * v.inter_stride + ((size_t)u * TILES * N + y) * W;
-            float2* dst = rowp + (size_t)(jj / W) * N * W + (jj % W);
-            dst[(size_t)q * (NSL / W) * N * W] = val;
-        };
-        if constexpr (!S3) {
-            auto emit = [&](int m, int q, float2 val) {
-                int b, jj;
-                E::template bj<E::RL>((int)threadIdx.x + m * T, b, jj);
-                put(b, jj, q, val);
-            };
-            E::run_regs(in, lds, tws, emit);
-        } else {
-#pragma unroll
-            for (int p = 0; p < 4; ++p) Idft<R0>::run(&in[p * R0]);
-            if constexpr (SHARE && !XSEP) __syncthreads();  // every lane has read the exchange off the image
-            // pass 0: Q1..Q3 (sequence slot 3 idle); row 0 only, pass 1: srow's input in slot 0
-            for (int ps = 0; ps < (y == 0 ? 2 : 1); ++ps) {
-#pragma unroll
-                for (int p = 0; p < 3; ++p) {
-                    if (ps && p) continue;
-                    float2* dst = lds + E::lidx(p, j * R0);
-#pragma unroll
-                    for (int q = 0; q < R0; ++q) dst[E::loff(q, 1)] = in[(ps ? 3 : p) * R0 + q];
-                }
-                __syncthreads();
-                auto emit = [&](int m, int q, float2 val) {
-                    int b, jj;
-                    E::template bj<E::RL>((int)threadIdx.x + m * T, b, jj);
-                    put(ps ? 3 : b, jj, q, val);
-                };
-                E::template stages_from<1>(lds, tws, emit, ps ? 1 : 3);
-                if (y == 0) __syncthreads();  // LDS reused by pass 1
-            }
-        }
-        __syncthreads();
-        if (!EARLY_PF && next < total_rows) load(next, h);
-    }
-}
-
-// Pass A3P (N = 4096, column parity b = v.xpar, ocean_set_column_parity): the row pass of a rank
-// that owns the columns x = 2m + b.  With X[x] = sum_n a[n] e^{2 pi i n x / N} and n = n' + (N/2) h,
-//   X[2m + b] = sum_{n' < N/2} z_b[n'] e^{2 pi i n' m / (N/2)},  z_b[n'] = (a[n'] + (-1)^b a[n' + N/2]) w_N^{b n'}
-// (decimation in frequency), so the rank evolves the whole row (its h0 is read whole either way),
-// forms z_b of each of the four sequences with one radix-2 butterfly in registers and runs an
-// N/2-point transform instead of the N-point one: half the butterflies and LDS traffic of pass A3Q.
-// Lane j (N/8 lanes) evolves texels j + r N/8, r < 8; texels r and r + 4 give z_b[j + r N/8], r < 4:
-// stage-0 butterfly j of the N/2-point plan with first radix 4 (the engine of pass A3Q at N/2).
-// Outputs m < N/2 go to intermediate column m (compact); srow likewise.  d0 is per row (texel 0).
-// SHARE: texel x and its row mirror N - x have the same |k| (nx negated), so the same 1/|k|, omega
-// and phase factor e = exp(i omega t): lane j computes them for its texels r < 4 and reads those of
-// r >= 4 from the lane that owns the mirrors (512 - j, r' = 7 - r; lane 0: r' = 8 - r, and x = N/2
-// itself) through an LDS exchange -- half the square roots, divisions and sincos of the evolve (pass
-// A3P issues ~190 VALU per texel against ~175 for pass AQ's full-length transforms, SQ counters).
-// The exchanged 1/|k| is a hardware reciprocal (1 ulp; omega stays correctly rounded, the phase
-// omega t of large t depends on it), and the srow sequence is formed on row 0 only.
-template <int N, bool EARLY_PF = A3P_EARLY_PF, bool SHARE = true>
-__global__ __launch_bounds__(N / 8) A3P_WPEU void k_pass_a3p(DevView v, float time, int total_rows) {
-    constexpr int H = N / 2;  // transform length
-    constexpr int FIRST = 4;
-    using TW = StageTwCompactSub<H, N, FIRST>;
-    using E = Engine<H, 4, false, true, FIRST, TW>;
-    constexpr int T = E::THREADS;
-    constexpr int R0 = E::R0;
-    constexpr int NJ = H / R0;  // lanes = texel stride
-    constexpr int W = inter_w(N);
-    constexpr int TILES = N / W;
-    constexpr int NSL = H / E::RL;
-    static_assert(T == NJ && R0 == 4 && T == N / 8, "lane j <-> stage-0 butterfly j of each sequence");
-    __shared__ float2 lds[E::LDS_ELEMS];
-    __shared__ float2 twl[TW::kLdsEntries];
-    __shared__ float4 xch[SHARE ? R0 * NJ : 1];  // (e.x, e.y, 1/|k|, -) of texel j + r NJ at [r][j]
-    TW::load(twl, v.tw, threadIdx.x, T);
-    const float2* tws = twl;
-    __shared__ WaveBand band[kMaxCascades];
-    if ((int)threadIdx.x < v.C) band[threadIdx.x] = wave_band(v.casc + threadIdx.x * 5);
-    const int j = (int)threadIdx.x;
-    const bool j0 = (j == 0);
-    const int jm = (NJ - j) & (NJ - 1);  // lane of the mirrors (r' = 7 - r; lane 0: 8 - r)
-    const int par = v.xpar;
-    const float sgn = par ? -1.0f : 1.0f;
-    float4 h[2 * R0];
-    auto load = [&](int item, float4* hh) {
-        const Win w = make_win(v.h0 + (size_t)item * N, (unsigned)(N * 16));
-#pragma unroll
-        for (int r = 0; r < 2 * R0; ++r) hh[r] = bload4(w, j * 16, r * NJ * 16);
-    };
-    // twiddles w_N^{b n'} of the lane's z elements n' = j + r NJ (b = 1; 1 for b = 0)
-    float2 zt[R0];
-#pragma unroll
-    for (int r = 0; r < R0; ++r) zt[r] = par ? v.tw[j + r * NJ] : make_float2(1.0f, 0.0f);
-    // the shared per-texel factors of texel x of row y: (e.x, e.y, 1/|k|)
-    auto factors = [&](int x, int y, const WaveBand& wb) {
-        const int nx = x - N / 2, nz = y - N / 2;
-        const float kx = (float)nx * wb.dk, kz = (float)nz * wb.dk;
-        const float kmag = sqrtf(kx * kx + kz * kz);
-        if (!(kmag >= wb.lo && kmag <= wb.hi)) return make_float4(1.0f, 0.0f, 1.0f, 0.0f);
-        const Phase e = evolve_phase(sqrtf(v.gravity * kmag), time);
-        return make_float4(e.ex, e.ey, __builtin_amdgcn_rcpf(kmag), 0.0f);
-    };
-    int item = (gridDim.x % 8 == 0) ? (int)(blockIdx.x % 8) * (int)(gridDim.x / 8) + (int)blockIdx.x / 8
-                                    : (int)blockIdx.x;
-    if (item < total_rows) load(item, h);
-    __syncthreads();  // twiddles, band
-    for (; item < total_rows; item += gridDim.x) {
-        const int u = item / N, y = item % N;
-        const WaveBand wb = band[(u + v.c0) % v.C];
-        float4 own[SHARE ? R0 : 1];
-        if constexpr (SHARE) {
-#pragma unroll
-            for (int r = 0; r < R0; ++r) {
-                own[r] = factors(j + r * NJ, y, wb);
-                xch[r * NJ + j] = own[r];
-            }
-            __syncthreads();
-        }
-        float2 in[4 * R0];  // slot p * R0 + r: sequence p, stage-0 input r (z_b[j + r NJ])
-#pragma unroll
-        for (int r = 0; r < R0; ++r) {
-            float2 qv[2][4];  // texel j + r NJ (lo) and j + (r + 4) NJ (hi): Q1..Q3 and row 0's Q4
-#pragma unroll
-            for (int hi = 0; hi < 2; ++hi) {
-                const int rr = r + hi * R0;
-                float4 wd;
-                Phase ph;
-                if constexpr (SHARE) {
-                    float4 f;
-                    if (hi == 0) {
-                        f = own[r];
-                    } else {
-                        const int rp = j0 ? 2 * R0 - rr : 2 * R0 - 1 - rr;  // the mirror's r' (< 4, or 4 on lane 0)
-                        f = (rp < R0) ? xch[(rp & (R0 - 1)) * NJ + jm] : factors(j + rr * NJ, y, wb);
-                    }
-                    const float kx = (float)(j + rr * NJ - N / 2) * wb.dk, kz = (float)(y - N / 2) * wb.dk;
-                    wd = make_float4(kx, f.z, kz, 0.0f);
-                    ph.ex = f.x;
-                    ph.ey = f.y;
-                } else {
-                    wd = wave_data(j + rr * NJ, y, N, wb, v.gravity);
-                    ph = evolve_phase(wd.w, time);
-                }
-                const float2 hh = evolve_h(h[rr], ph);
-                QTex qa, qb;
-                qv[hi][3] = make_float2(0.0f, 0.0f);
-                if (y != 0 && !(rr == 0 && j0)) {
-                    q_fast(hh, wd, qa, qb);
-                } else {  // Nyquist lines (see pass AQ)
-                    const float4 wm = make_float4((j0 && rr == 0) ? wd.x : -wd.x, wd.y, y ? -wd.z : wd.z, wd.w);
-                    const Planes4 o = planes_of(hh, wd), om = planes_of(make_float2(hh.x, -hh.y), wm);
-                    q_planes(o, om, qa, qb);
-                    if (y == 0) qv[hi][3] = q4_full(o, om);
-                    if (rr == 0 && j0) q_side(v, u)[y] = q4_minus(o, om, wd.z);
-                }
-#pragma unroll
-                for (int p = 0; p < 3; ++p) qv[hi][p] = qa.q[p];
-            }
-#pragma unroll
-            for (int p = 0; p < 4; ++p) {
-                if (SHARE && p == 3 && y != 0) {  // srow's sequence exists on row 0 only
-                    in[p * R0 + r] = make_float2(0.0f, 0.0f);
-                    continue;
-                }
-                const float2 zs = make_float2(qv[0][p].x + sgn * qv[1][p].x, qv[0][p].y + sgn * qv[1][p].y);
-                in[p * R0 + r] = par ? cmul(zs, zt[r]) : zs;
-            }
-        }
-        const int next = item + gridDim.x;
-        if (EARLY_PF && next < total_rows) load(next, h);  // the next row's h0 in flight across this row's stages
-        auto put = [&](int b, int jj, int q, float2 val) {
-            const int m = jj + q * NSL;  // compact column: x = 2 m + b
-            if (b == 3) {
-                if (y == 0) q_side(v, u)[N + m] = val;  // srow
-                return;
-            }
             float2* rowp = v.tplane + (size_t)b * v.inter_stride + ((size_t)u * TILES * N + y) * W;
             float2* dst = rowp + (size_t)(jj / W) * N * W + (jj % W);
             dst[(size_t)q * (NSL / W) * N * W] = val;
@@ -613,24 +345,30 @@ __global__ __launch_bounds__(N / 8) A3P_WPEU void k_pass_a3p(DevView v, float ti
             if (y == 0) __syncthreads();  // LDS reused by pass 1
         }
         __syncthreads();
-        if (!EARLY_PF && next < total_rows) load(next, h);
     }
 }
 
-// Pass A3PP (N = 4096, column parity b, ocean_set_column_parity; OCEAN_A3P_PAIR=1): pass A3P on
-// mirror-pair rows, as pass AQ pairs them.  Item i of a unit is row y1 = i with y2 = (N - i) % N;
-// lane j loads h0k of texels x_r = j + r N/8 (r < 8) of row y1 and of their mirrors N - x_r in row
-// y2 (8 B per texel instead of pass A3P's 16: h(-k) = conj h(k) from the pair), evaluates the
-// shared factors once per texel pair (and, through the LDS exchange, once per four texels: x and
-// N - x of row y1 share them too), and folds z_b for both rows: row y1 at stage-0 butterfly j, row
-// y2 at butterfly jm = (N/8 - j) % (N/8).  Eight sequence slots, two radix-16 butterflies per lane
-// per LDS stage: 0-2 Q1..Q3 of row y1, 3-5 of row y2, 6 row 0's srow, 7 idle.  The self-mirror rows
-// 0 and N/2 run the same code; their y2 slots duplicate y1 and are not stored.
-// FIRST = 2 (OCEAN_A3P_PAIR=3/4): N/4 lanes, texels j + r N/4 (r < 4), a radix-2 first stage and one
-// radix-16 butterfly per lane per LDS stage -- 16 waves per workgroup instead of 8.
-template <int N, bool EARLY_PF = true, int FIRST = 4>
-__global__ __launch_bounds__(N / (2 * FIRST)) void k_pass_a3pp(DevView v, float time, int items) {
+// Pass A3PP (N = 4096, column parity b = v.xpar, ocean_set_column_parity): the row pass of a rank that
+// owns the columns x = 2m + b.  With X[x] = sum_n a[n] e^{2 pi i n x / N} and n = n' + (N/2) h,
+//   X[2m + b] = sum_{n' < N/2} z_b[n'] e^{2 pi i n' m / (N/2)},  z_b[n'] = (a[n'] + (-1)^b a[n' + N/2]) w_N^{b n'}
+// (decimation in frequency), so the rank evolves the whole row (its h0k is read whole either way), forms
+// z_b of each sequence with one radix-2 butterfly in registers and runs an N/2-point transform instead
+// of the N-point one.  Rows are paired as pass AQ pairs them: item i of a unit is row y1 = i with
+// y2 = (N - i) % N; lane j (N/4 lanes) loads h0k of texels x_r = j + r N/4 (r < 4) of row y1 and of
+// their mirrors N - x_r in row y2 (h(-k) = conj h(k) from the pair), evaluates the per-texel factors
+// once per texel pair and, through an LDS exchange, once per four texels (x and N - x of row y1 have the
+// same |k|: 1/|k| from the hardware reciprocal, omega correctly rounded), and folds z_b for both rows:
+// row y1 at stage-0 butterfly j, row y2 at butterfly jm = (N/4 - j) % (N/4).  The 2048-point plan starts
+// with a radix-2 stage (2, 16, 16, 4), so each LDS stage has one radix-16 butterfly per lane (16 waves
+// per workgroup).  Seven sequence slots: 0-2 Q1..Q3 of row y1, 3-5 of row y2, 6 row 0's srow.  The
+// self-mirror rows 0 and N/2 run the same code; their y2 slots duplicate y1 and are not stored.  Outputs
+// m < N/2 go to intermediate column m (compact); d0 is per row (texel 0).  The next pair's h0k is in
+// flight across the stages (0.094 against 0.098 ms loaded after them).  OFF32: 32-bit byte offsets from
+// the intermediate's base (host-checked < 4 GiB), else 64-bit addresses.
+template <int N, bool OFF32 = true>
+__global__ __launch_bounds__(N / 4) void k_pass_a3pp(DevView v, float time, int items) {
     constexpr int H = N / 2;  // transform length
+    constexpr int FIRST = 2;
     using TW = StageTwCompactSub<H, N, FIRST>;
     using E = Engine<H, 8, false, true, FIRST, TW, 8 * FIRST>;
     constexpr int T = E::THREADS;
@@ -640,7 +378,7 @@ __global__ __launch_bounds__(N / (2 * FIRST)) void k_pass_a3pp(DevView v, float 
     constexpr int TILES = N / W;
     constexpr int NSL = H / E::RL;
     constexpr int IPU = N / 2 + 1;  // items per unit
-    static_assert(T == NJ && R0 == FIRST && T == N / (2 * FIRST), "lane j <-> stage-0 butterfly j of every slot");
+    static_assert(T == NJ && R0 == FIRST && T == N / 4, "lane j <-> stage-0 butterfly j of every slot");
     __shared__ __align__(16) float2 lds[E::LDS_ELEMS];
     __shared__ float2 twl[TW::kLdsEntries];
     static_assert(R0 * NJ * 16 <= E::LDS_ELEMS * 8, "the factor exchange fits the idle image");
@@ -654,24 +392,14 @@ __global__ __launch_bounds__(N / (2 * FIRST)) void k_pass_a3pp(DevView v, float 
     const int jm = (NJ - j) & (NJ - 1);
     const int par = v.xpar;
     const float sgn = par ? -1.0f : 1.0f;
-    // iteration r (texel pairs r, r + 4) folds z of row y1 at slot r and of row y2 at slot i2(r)
-    auto i2 = [&](int r) { return j0 ? ((R0 - r) & (R0 - 1)) : (R0 - 1 - r); };
-    // w_N^{b n'} at n' = j + r NJ (row y1) and jm + i2(r) NJ (row y2), by iteration r.  FIRST = 2: NJ = N/4,
-    // w_N^{n + N/4} = i w_N^n, so two values and a quarter turn (8 VGPRs fewer at 128)
-    constexpr int NZ = FIRST == 2 ? 1 : R0;
-    float2 zt1[NZ], zt2[NZ];
-#pragma unroll
-    for (int r = 0; r < NZ; ++r) {  // FIRST = 2: zt1[0] = w^j, zt2[0] = w^jm
-        zt1[r] = par ? v.tw[j + r * NJ] : make_float2(1.0f, 0.0f);
-        zt2[r] = par ? v.tw[jm + (FIRST == 2 ? 0 : i2(r)) * NJ] : make_float2(1.0f, 0.0f);
-    }
-    auto z1_at = [&](int r) {
-        if constexpr (FIRST == 2) return (r && par) ? cmul_i(zt1[0]) : zt1[0];
-        else return zt1[r];
-    };
-    auto z2_at = [&](int r) {  // i2(r) = 1 - r off lane 0, r on lane 0
-        if constexpr (FIRST == 2) return (i2(r) && par) ? cmul_i(zt2[0]) : zt2[0];
-        else return zt2[r];
+    // w_N^{b n'} at n' = j + r NJ (row y1) and jm + r NJ (row y2): NJ = N/4 and w_N^{n + N/4} = i w_N^n, so
+    // two values and a quarter turn
+    const float2 zt1 = par ? v.tw[j] : make_float2(1.0f, 0.0f);
+    const float2 zt2 = par ? v.tw[jm] : make_float2(1.0f, 0.0f);
+    auto z1_at = [&](int r) { return (r && par) ? cmul_i(zt1) : zt1; };
+    auto z2_at = [&](int r) {  // slot i2(r) = 1 - r off lane 0, r on lane 0
+        const int i2 = j0 ? r : 1 - r;
+        return (i2 && par) ? cmul_i(zt2) : zt2;
     };
     auto rows_of = [&](int it, int& u, int& y1, int& y2) {
         u = it / IPU;
@@ -742,8 +470,8 @@ __global__ __launch_bounds__(N / (2 * FIRST)) void k_pass_a3pp(DevView v, float 
                     qb[hi][p] = b.q[p];
                 }
             }
-            // row y1: z[j + r NJ] = Q(x_r) + s Q(x_{r+4});  row y2 (slot i2(r)): Q(N - x_{r+4}) + s Q(N - x_r),
-            // except lane 0, r = 0 (texels 0 and N/2 map onto themselves): Q(N - x_0) + s Q(N - x_4)
+            // row y1: z[j + r NJ] = Q(x_r) + s Q(x_{r+R0});  row y2 (slot i2(r)): Q(N - x_{r+R0}) + s Q(N - x_r),
+            // except lane 0, r = 0 (texels 0 and N/2 map onto themselves): Q(N - x_0) + s Q(N - x_R0)
             const bool swap2 = j0 && r == 0;
 #pragma unroll
             for (int p = 0; p < 4; ++p) {
@@ -771,17 +499,17 @@ __global__ __launch_bounds__(N / (2 * FIRST)) void k_pass_a3pp(DevView v, float 
             }
         }
         const int next = it + gridDim.x;
-        if (EARLY_PF && next < items) load_pair(next);  // the next pair's h0k in flight across the stages
+        if (next < items) load_pair(next);  // the next pair's h0k in flight across the stages
 #pragma unroll
-        for (int s = 0; s < 7; ++s) Idft<R0>::run(in[s]);
+        for (int sl = 0; sl < 7; ++sl) Idft<R0>::run(in[sl]);
         __syncthreads();  // every lane has read the exchange off the image
         const int live = (y1 == 0) ? 7 : 6;
 #pragma unroll
-        for (int s = 0; s < 7; ++s) {
-            if (s == 6 && y1 != 0) continue;
-            float2* dst = lds + E::lidx(s, ((s >= 3 && s < 6) ? jm : j) * R0);
+        for (int sl = 0; sl < 7; ++sl) {
+            if (sl == 6 && y1 != 0) continue;
+            float2* dst = lds + E::lidx(sl, ((sl >= 3 && sl < 6) ? jm : j) * R0);
 #pragma unroll
-            for (int q = 0; q < R0; ++q) dst[E::loff(q, 1)] = in[s][q];
+            for (int q = 0; q < R0; ++q) dst[E::loff(q, 1)] = in[sl][q];
         }
         __syncthreads();
         auto emit = [&](int m, int q, float2 val) {
@@ -794,20 +522,19 @@ __global__ __launch_bounds__(N / (2 * FIRST)) void k_pass_a3pp(DevView v, float 
             }
             if (b >= 3 && self) return;  // the self-mirror row's duplicate
             const int p = b >= 3 ? b - 3 : b;
-            if constexpr (FIRST == 2) {  // 32-bit byte offsets from the intermediate's base (host-checked < 4 GiB)
-                const unsigned e = (unsigned)p * (unsigned)v.inter_stride +
-                                   ((unsigned)u * TILES * N + (unsigned)(b >= 3 ? y2 : y1)) * W +
+            const int y = b >= 3 ? y2 : y1;
+            if constexpr (OFF32) {
+                const unsigned e = (unsigned)p * (unsigned)v.inter_stride + ((unsigned)u * TILES * N + (unsigned)y) * W +
                                    (unsigned)(jj / W) * N * W + (unsigned)(jj % W) + (unsigned)q * (NSL / W) * N * W;
                 *(float2*)((char*)v.tplane + (store_off_t)(e * 8u)) = val;
             } else {
-                float2* rowp = v.tplane + (size_t)p * v.inter_stride + ((size_t)u * TILES * N + (b >= 3 ? y2 : y1)) * W;
-                float2* dst = rowp + (size_t)(jj / W) * N * W + (jj % W);
+                float2* dst = v.tplane + (size_t)p * v.inter_stride + ((size_t)u * TILES * N + y) * W +
+                              (size_t)(jj / W) * N * W + (jj % W);
                 dst[(size_t)q * (NSL / W) * N * W] = val;
             }
         };
         E::template stages_from<1>(lds, tws, emit, live);
         __syncthreads();
-        if (!EARLY_PF && next < items) load_pair(next);
     }
 }
 
@@ -955,49 +682,43 @@ __global__ __launch_bounds__((WT ? WT : b3_w(N)) * N / kElems) void k_pass_bq(De
     }
 }
 
-int env_int_q(const char* name, int dflt) {
-    const char* e = std::getenv(name);
-    return e ? std::atoi(e) : dflt;
-}
-
 template <class K>
 int grid_q(K kernel, int threads, int items) {
     const int g = device_cus() * resident_per_cu((const void*)kernel, threads);
     return items < g ? items : g;
 }
 
-template <int N, bool BAND = false, int WT = 0>
+// Byte offsets of a store into the chunk's intermediate planes 0..2 fit 32 bits (k_pass_aq /
+// k_pass_a3pp OFF32): the last byte of plane 2 lies below 4 GiB from the base.
+bool inter_off32(const DevView& v) { return ((size_t)2 * v.inter_stride + v.inter_stride) * 8 <= ((size_t)1 << 32); }
+
+template <int N, bool BAND = false, int WT = 0, bool OFF32 = true>
 hipError_t go_aq(const DevView& v, float t, hipStream_t s) {
     if constexpr (WT == 0) {
-        if (v.tile_w != inter_w(N)) return go_aq<N, BAND, 4>(v, t, s);
+        if (v.tile_w != inter_w(N)) return go_aq<N, BAND, 4, OFF32>(v, t, s);
     }
     if constexpr (!BAND) {
-        if (v.nx != N) return go_aq<N, true, WT>(v, t, s);
+        if (v.nx != N) return go_aq<N, true, WT, OFF32>(v, t, s);
+    }
+    if constexpr (OFF32) {
+        if (!inter_off32(v)) return go_aq<N, BAND, WT, false>(v, t, s);
     }
     constexpr int T = N / 4;
     const int items = v.units * (N / 2 + 1);
-    const int g = grid_q(k_pass_aq<N, BAND, WT>, T, items);
-    launch((k_pass_aq<N, BAND, WT>), dim3(g), dim3(T), 0, s, v, t, items);
+    const int g = grid_q(k_pass_aq<N, BAND, WT, OFF32>, T, items);
+    launch((k_pass_aq<N, BAND, WT, OFF32>), dim3(g), dim3(T), 0, s, v, t, items);
     return hipGetLastError();
 }
 
-template <int N, bool BAND = false, bool S3 = true, bool PF = true, bool SLIM = false, bool SHARE = false>
+template <int N, bool BAND = false>
 hipError_t go_a3q(const DevView& v, float t, hipStream_t s) {
-    if constexpr (S3 && PF && !SLIM && !SHARE) {
-        static const int s3 = env_int_q("OCEAN_A3Q_S3", 1);  // 0: the four-sequence stages on every row (A/B)
-        static const int pf = env_int_q("OCEAN_A3Q_PF", 1);  // 0: next row's h0 loaded after the stages (A/B)
-        static const int sh = env_int_q("OCEAN_A3Q_SHARE", 0);  // 1: mirror factors exchanged (A/B)
-        if (!s3) return go_a3q<N, BAND, false, PF>(v, t, s);
-        if (!pf) return go_a3q<N, BAND, S3, false>(v, t, s);
-        if (sh) return go_a3q<N, BAND, S3, PF, false, true>(v, t, s);
-    }
     if constexpr (!BAND) {
-        if (v.nx != N) return go_a3q<N, true, S3, PF, SLIM, SHARE>(v, t, s);
+        if (v.nx != N) return go_a3q<N, true>(v, t, s);
     }
     constexpr int T = N / 4;
     const int total = v.units * N;
-    const int g = grid_q(k_pass_a3q<N, BAND, S3, PF, SLIM, SHARE>, T, total);
-    launch((k_pass_a3q<N, BAND, S3, PF, SLIM, SHARE>), dim3(g), dim3(T), 0, s, v, t, total);
+    const int g = grid_q(k_pass_a3q<N, BAND>, T, total);
+    launch((k_pass_a3q<N, BAND>), dim3(g), dim3(T), 0, s, v, t, total);
     return hipGetLastError();
 }
 
@@ -1021,77 +742,26 @@ hipError_t go_bq(const DevView& v, hipStream_t s) {
 
 // N = 2048 keeps the four-plane passes: pass A3Q's idle fourth sequence slot costs more there
 // than the column passes save (4 x 2048^2: 612 against 599 us per frame).
-bool pass_q_supported(int n, int planes) {
-    static const int q2048 = env_int_q("OCEAN_Q2048", 0);
-    return planes == 4 && (n == 512 || n == 1024 || n == 4096 || (n == 2048 && q2048));
-}
-
-// Row pass of a column-parity shard (OCEAN_A3P_PAIR): 3 (default) pass A3PP on 1024 lanes with the
-// next pair's h0k in flight across the stages (7 VGPRs spilled; 0.094 against 0.098 ms); 4 the same
-// with it loaded after the stages; 1 / 2 pass A3PP on 512 lanes (early / late); 0 pass A3P (one row
-// per item, full h0).  Pass A3PP needs a valid h0k (the caller passes a null h0k after an H0 upload,
-// and pass A3P runs).
-int pass_a3p_pair_mode() {
-    static const int pair = env_int_q("OCEAN_A3P_PAIR", 3);
-    return pair;
-}
+bool pass_q_supported(int n, int planes) { return planes == 4 && (n == 512 || n == 1024 || n == 4096); }
 
 hipError_t launch_pass_a_q(const DevView& v, float t, hipStream_t s) {
     if (!pass_q_supported(v.n, v.planes) || !v.qside) return hipErrorInvalidValue;
-    if (v.xstr == 2) {  // column parity (even / odd columns of every row)
-        if (v.n != 4096 || v.x0 != 0 || v.nx != v.n / 2) return hipErrorInvalidValue;
-        constexpr int T = 4096 / 8;
-        const int total = v.units * 4096;
-        const int pair = pass_a3p_pair_mode();
-        if (pair && v.h0k) {
-            const int items = v.units * (4096 / 2 + 1);
-            // 1024 lanes, radix-2 first stage (early / late next-pair h0k); its stores take 32-bit byte
-            // offsets, so the three intermediate planes must lie within 4 GiB of the base (else 512 lanes)
-            const bool off32 = (size_t)v.inter_stride * 3 * 8 < ((size_t)1 << 32);
-            if ((pair == 3 || pair == 4) && off32) {
-                constexpr int T2 = 4096 / 4;
-                if (pair == 4) {
-                    const int g = grid_q(k_pass_a3pp<4096, false, 2>, T2, items);
-                    launch((k_pass_a3pp<4096, false, 2>), dim3(g), dim3(T2), 0, s, v, t, items);
-                } else {
-                    const int g = grid_q(k_pass_a3pp<4096, true, 2>, T2, items);
-                    launch((k_pass_a3pp<4096, true, 2>), dim3(g), dim3(T2), 0, s, v, t, items);
-                }
-                return hipGetLastError();
-            }
-            if (pair == 2) {  // next pair's h0k loaded after the stages
-                const int g = grid_q(k_pass_a3pp<4096, false>, T, items);
-                launch((k_pass_a3pp<4096, false>), dim3(g), dim3(T), 0, s, v, t, items);
-                return hipGetLastError();
-            }
-            const int g = grid_q(k_pass_a3pp<4096>, T, items);
-            launch((k_pass_a3pp<4096>), dim3(g), dim3(T), 0, s, v, t, items);
-            return hipGetLastError();
+    if (v.xstr == 2) {  // column parity (even / odd columns of every row): pass A3PP on mirror-pair rows
+        if (v.n != 4096 || v.x0 != 0 || v.nx != v.n / 2 || !v.h0k) return hipErrorInvalidValue;
+        constexpr int T = 4096 / 4;
+        const int items = v.units * (4096 / 2 + 1);
+        if (inter_off32(v)) {
+            const int g = grid_q(k_pass_a3pp<4096, true>, T, items);
+            launch((k_pass_a3pp<4096, true>), dim3(g), dim3(T), 0, s, v, t, items);
+        } else {
+            const int g = grid_q(k_pass_a3pp<4096, false>, T, items);
+            launch((k_pass_a3pp<4096, false>), dim3(g), dim3(T), 0, s, v, t, items);
         }
-        static const int share = env_int_q("OCEAN_A3P_SHARE", 1);  // 0: every texel evaluates its own factors (A/B)
-        if (!share) {
-            const int g = grid_q(k_pass_a3p<4096, A3P_EARLY_PF, false>, T, total);
-            launch((k_pass_a3p<4096, A3P_EARLY_PF, false>), dim3(g), dim3(T), 0, s, v, t, total);
-            return hipGetLastError();
-        }
-        const int g = grid_q(k_pass_a3p<4096>, T, total);
-        launch((k_pass_a3p<4096>), dim3(g), dim3(T), 0, s, v, t, total);
         return hipGetLastError();
     }
-    // OCEAN_AQ_ROWS=1: the one-row-per-item pass A3Q at N = 1024 (full h0, 16 B per texel) instead of the
-    // mirror-pair pass AQ (h0k, 8 B per texel); A/B
-    static const int aq_rows = env_int_q("OCEAN_AQ_ROWS", 0);
-    static const int aq_rows_pf = env_int_q("OCEAN_AQ_ROWS_PF", 1);
-    if (aq_rows == 1 && v.n == 1024) return aq_rows_pf ? go_a3q<1024>(v, t, s) : go_a3q<1024, false, true, false>(v, t, s);
-    if (aq_rows == 2 && v.n == 1024)  // slim image
-        return aq_rows_pf ? go_a3q<1024, false, true, true, true>(v, t, s) : go_a3q<1024, false, true, false, true>(v, t, s);
-    if (aq_rows == 3 && v.n == 1024)  // slim image, mirror factors exchanged
-        return aq_rows_pf ? go_a3q<1024, false, true, true, true, true>(v, t, s)
-                          : go_a3q<1024, false, true, false, true, true>(v, t, s);
     switch (v.n) {
         case 512: return v.h0k ? go_aq<512>(v, t, s) : hipErrorInvalidValue;
         case 1024: return v.h0k ? go_aq<1024>(v, t, s) : hipErrorInvalidValue;
-        case 2048: return go_a3q<2048>(v, t, s);
         case 4096: return go_a3q<4096>(v, t, s);
     }
     return hipErrorInvalidValue;

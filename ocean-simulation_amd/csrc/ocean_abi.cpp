@@ -55,10 +55,6 @@ const void*& last_kernel() {
     thread_local const void* slot = nullptr;
     return slot;
 }
-int& last_kernel_nargs() {
-    thread_local int n = 0;
-    return n;
-}
 
 namespace {
 std::mutex g_occ_mu;
@@ -112,8 +108,11 @@ struct StagePool {
     std::mutex mu;
     std::vector<void*> free_slots, all;
     ~StagePool() {
+        int prev = 0;
+        const bool had = hipGetDevice(&prev) == hipSuccess;
         (void)hipSetDevice(device);
         for (void* p : all) (void)hipFree(p);
+        if (had) (void)hipSetDevice(prev);  // the caller's current device is left as it was
     }
     hipError_t take(void** out) {
         std::lock_guard<std::mutex> lk(mu);
@@ -134,6 +133,30 @@ struct StagePool {
     }
 };
 
+// Environment knobs of a context, read once in ocean_create ("Environment knobs";
+// tests/test_abi.py checks that this is every getenv of the library).  The defaults are the measured
+// best; every knob changes the schedule only, never the arithmetic of a texel, except OCEAN_Q and
+// OCEAN_A4, which select the reference's four-plane passes (within the fp32 tolerance / bit-identical).
+struct ocean_options {
+    int q = 1;              // OCEAN_Q=0: the four-plane fused frame where the three-plane one applies
+    int a4 = 1;             // OCEAN_A4=0: the per-texel row pass A3 instead of the mirror-pair pass A4
+    long chunk_mib = 192;   // OCEAN_CHUNK_MIB: intermediate MiB per unit chunk of a frame (0: whole frame)
+    int c4_bands = 0;       // OCEAN_C4_BANDS: N >= 2048 column passes per (unit, band); 0 = auto
+    long op_chunk_mib = 0;  // OCEAN_OP_CHUNK_MIB: MiB of unit-planes per chunk of ocean_ifft2d (0: auto)
+    int tile_w = 0;         // OCEAN_TILE_W: column-tile width of the fused path at N = 128..1024 (0: auto)
+
+    static ocean_options from_env() {
+        ocean_options o;
+        if (const char* e = std::getenv("OCEAN_Q")) o.q = std::atoi(e);
+        if (const char* e = std::getenv("OCEAN_A4")) o.a4 = std::atoi(e);
+        if (const char* e = std::getenv("OCEAN_CHUNK_MIB")) o.chunk_mib = std::max(0L, std::atol(e));
+        if (const char* e = std::getenv("OCEAN_C4_BANDS")) o.c4_bands = std::max(0, std::atoi(e));
+        if (const char* e = std::getenv("OCEAN_OP_CHUNK_MIB")) o.op_chunk_mib = std::max(0L, std::atol(e));
+        if (const char* e = std::getenv("OCEAN_TILE_W")) o.tile_w = std::max(0, std::atoi(e));
+        return o;
+    }
+};
+
 struct ocean_ctx {
     int device = 0;
     int n = 0, logn = 0, C = 0, T = 0, P = 4;
@@ -142,22 +165,12 @@ struct ocean_ctx {
     // device buffers
     float2* noise = nullptr;
     float4* h0 = nullptr;
-    float2* h0k = nullptr;   // h0.xy for the mirror-pair row pass (pass_a4_supported sizes)
+    float2* h0k = nullptr;   // h0.xy for the mirror-pair row passes: pass_a4_supported sizes, and pass A3PP
+                             // at N = 4096 (allocated by ocean_set_column_parity)
     bool h0k_valid = false;  // h0k matches h0 (false after ocean_write(H0): .zw may then be arbitrary)
     bool h0_conj = false;    // h0.zw = conj h0(-k) (from ocean_init_spectrum; the three-plane frame needs it)
-    int a4 = 1;              // OCEAN_A4=0 selects the v3 row pass
-    int q = 1;               // OCEAN_Q=0: the four-plane fused frame where the three-plane one applies (A/B)
-    long chunk_mib = 192;    // OCEAN_CHUNK_MIB: intermediate MiB per unit chunk (step_fused)
-    int c4_bands = 0;        // OCEAN_C4_BANDS: N >= 2048 column passes per (unit, band); 0 = auto
-    int chunk_min = 1 << 30; // OCEAN_CHUNK_MIN: units per chunk when one unit exceeds OCEAN_CHUNK_MIB
-    int chunk_reuse = 1;     // OCEAN_CHUNK_REUSE=0: one intermediate region per unit (A/B)
-    int op_four_step = 0;    // OCEAN_OP_FOUR_STEP=1: ocean_ifft2d at N >= 2048 through four-step columns (A/B)
-    int op_fold = -1;        // OCEAN_OP_FOLD: ocean_ifft2d at N >= 2048 through folded 1024-point columns
-                             // (-1 auto: N = 4096; 0 off: XCD-grouped whole-column tiles; 1 on at 2048 too)
-    int op_fold_cols = 8;    // OCEAN_FOLD_COLS: column-tile width of the folded columns (8 paired, or 16; A/B)
-    int op_fold_f = 2;       // OCEAN_FOLD_F: rows folded per column at 4096 (2: 2048-point columns, 4: 1024-point)
-    long op_chunk_mib = 0;   // OCEAN_OP_CHUNK_MIB: MiB of unit-planes per chunk of the operator IFFT (0: auto)
-    size_t inter_units = 0;  // units the intermediate holds (a chunk's, or all with chunk_reuse = 0)
+    ocean_options opt;       // environment knobs, read once in ocean_create
+    size_t inter_units = 0;  // units the intermediate holds (one chunk of a frame; every chunk reuses it)
     int band_x0 = 0, band_nx = 0;  // column band of the fused passes (ocean_set_column_band); nx = n: whole
     int col_par = -1;              // column parity (ocean_set_column_parity): -1 off, else x = 2 m + col_par
     int tile_w = 8;                // column-tile width of the fused path's tile-major layouts (ocean_create)
@@ -193,19 +206,6 @@ struct ocean_ctx {
     double kind_ms[3] = {0, 0, 0};
     long long kind_count[3] = {0, 0, 0};
     const void* kind_kernel[3] = {nullptr, nullptr, nullptr};  // last kernel launched per kind (ocean_kernel_name)
-    // OCEAN_GRAPH=1: ocean_step replays one captured hipGraph of the fused frame, the time argument of
-    // its pass-A kernel nodes updated per frame
-    int graph_mode = 0;
-    bool capturing = false;
-    std::vector<std::pair<const void*, int>> captured_time_kernels;  // (kernel, argument count), kind 0
-    struct FrameGraph {
-        hipGraph_t g = nullptr;
-        hipGraphExec_t exec = nullptr;
-        std::vector<std::pair<hipGraphNode_t, int>> tnodes;  // pass-A kernel nodes, argument count
-        int x0 = -1, nx = -1, par = -2;
-        bool q = false;
-    } fg;
-    bool graph_stale = false;  // the captured frame's arguments changed (init_spectrum, uploads)
     static constexpr size_t kMaxPending = 2048;  // timed launches held before folding into kind_ms
 
     size_t texels() const { return (size_t)n * n; }
@@ -302,11 +302,7 @@ int timed(ocean_ctx* ctx, int kind, F&& launch, const char* what) {
     ocean::last_kernel() = nullptr;
     if (!ctx->timing) {
         const hipError_t e = launch();
-        if (ocean::last_kernel()) {
-            ctx->kind_kernel[kind] = ocean::last_kernel();
-            if (ctx->capturing && kind == 0)
-                ctx->captured_time_kernels.emplace_back(ocean::last_kernel(), ocean::last_kernel_nargs());
-        }
+        if (ocean::last_kernel()) ctx->kind_kernel[kind] = ocean::last_kernel();
         return e == hipSuccess ? OCEAN_OK : hip_fail(e, what);
     }
     if (ctx->pending.size() >= ocean_ctx::kMaxPending) {
@@ -375,8 +371,6 @@ void free_all(ocean_ctx* c) {
         (void)hipEventDestroy(t.b);
     }
     for (auto e : c->event_pool) (void)hipEventDestroy(e);
-    if (c->fg.exec) (void)hipGraphExecDestroy(c->fg.exec);
-    if (c->fg.g) (void)hipGraphDestroy(c->fg.g);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     if (c->stream) (void)hipStreamDestroy(c->stream);
 }
@@ -429,18 +423,7 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
     c->P = (flags & OCEAN_F_DISPLACEMENT_ONLY) ? 2 : 4;
     c->noise_set.assign(n_tiles, false);
     c->band_nx = n;
-    if (const char* ka = std::getenv("OCEAN_A4")) c->a4 = std::atoi(ka);
-    if (const char* kq = std::getenv("OCEAN_Q")) c->q = std::atoi(kq);
-    if (const char* kc = std::getenv("OCEAN_CHUNK_MIB")) c->chunk_mib = std::atol(kc);
-    if (const char* kb = std::getenv("OCEAN_C4_BANDS")) c->c4_bands = std::max(0, std::atoi(kb));
-    if (const char* km = std::getenv("OCEAN_CHUNK_MIN")) c->chunk_min = std::max(1, std::atoi(km));
-    if (const char* kr = std::getenv("OCEAN_CHUNK_REUSE")) c->chunk_reuse = std::atoi(kr);
-    if (const char* kf = std::getenv("OCEAN_OP_FOUR_STEP")) c->op_four_step = std::atoi(kf);
-    if (const char* kd = std::getenv("OCEAN_OP_FOLD")) c->op_fold = std::atoi(kd);
-    if (const char* kw = std::getenv("OCEAN_FOLD_COLS")) c->op_fold_cols = std::atoi(kw);
-    if (const char* kf2 = std::getenv("OCEAN_FOLD_F")) c->op_fold_f = std::atoi(kf2) == 4 ? 4 : 2;
-    if (const char* kg = std::getenv("OCEAN_GRAPH")) c->graph_mode = std::atoi(kg);
-    if (const char* ko = std::getenv("OCEAN_OP_CHUNK_MIB")) c->op_chunk_mib = std::max(0L, std::atol(ko));
+    c->opt = ocean_options::from_env();
     // Width of the fused path's column tiles.  With fewer tiles than CUs (one 512^2
     // cascade: 32 tiles of 16 columns) pass B ran on an eighth of the chip, so small
     // jobs at N <= 512 take 4-column tiles (at N = 1024 pass A's
@@ -452,10 +435,8 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
             cus = 256;
         const long tiles = (long)n_cascades * n_tiles * (n / c->tile_w);
         if (n >= 128 && n <= 512 && tiles < cus) c->tile_w = 4;
-        if (const char* kw = std::getenv("OCEAN_TILE_W")) {
-            const int w = std::atoi(kw);
-            if (n >= 128 && n <= 1024 && (w == 4 || w == ocean::fftcore::inter_w(n))) c->tile_w = w;
-        }
+        const int w = c->opt.tile_w;
+        if (w && n >= 128 && n <= 1024 && (w == 4 || w == ocean::fftcore::inter_w(n))) c->tile_w = w;
     }
 
     auto alloc = [&](void** p, size_t bytes) -> bool {
@@ -466,8 +447,9 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
     bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
     ok = ok && alloc((void**)&c->noise, tex * c->T * 8);
     ok = ok && alloc((void**)&c->h0, tex * U * 16);
-    // h0k: the mirror-pair row passes (N = 512 / 1024; at 4096 the column-parity pass A3PP)
-    if (ocean::pass_a4_supported(n, c->P) || (n == 4096 && c->P == 4)) ok = ok && alloc((void**)&c->h0k, tex * U * 8);
+    // h0k: the mirror-pair row passes (N = 256 / 512 / 1024; at 4096 the column-parity pass A3PP allocates
+    // it in ocean_set_column_parity)
+    if (ocean::pass_a4_supported(n, c->P)) ok = ok && alloc((void**)&c->h0k, tex * U * 8);
     ok = ok && alloc((void**)&c->waves, tex * U * 16);
     ok = ok && alloc((void**)&c->plane[0], tex * U * 8 * c->P);  // planes contiguous (one descriptor in pass A)
     if (ok)
@@ -480,9 +462,8 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
     }
     // the intermediate holds a chunk of either schedule: P planes, or (three-plane frame) planes
     // Q1..Q3 plus the per-unit side arrays in the fourth plane's room (fftq.hip)
-    c->inter_units = c->chunk_reuse ? (size_t)std::max(chunk_units(c, c->P),
-                                                       ocean::pass_q_supported(n, c->P) ? chunk_units(c, q_planes(c)) : 1)
-                                    : U;
+    c->inter_units = (size_t)std::max(chunk_units(c, c->P),
+                                      ocean::pass_q_supported(n, c->P) ? chunk_units(c, q_planes(c)) : 1);
     ok = ok && alloc((void**)&c->tplane, tex * c->inter_units * 8 * c->P);
     if (ocean::pass_q_supported(n, c->P)) ok = ok && alloc((void**)&c->qside, c->inter_units * 2 * n * 8);
     if (flags & OCEAN_F_NORMALS) ok = ok && alloc((void**)&c->normal, tex * U * 16);
@@ -620,7 +601,6 @@ int ocean_init_spectrum(ocean_ctx* ctx) {
     ctx->spectrum_ready = true;
     ctx->h0k_valid = ctx->h0k != nullptr;
     ctx->h0_conj = true;
-    ctx->graph_stale = true;  // the kernels' DevView argument carries the active gravity
     return OCEAN_OK;
 }
 
@@ -654,57 +634,25 @@ int ocean_ifft2d(ocean_ctx* ctx, int plane_mask) {
         }
         int np = 1;  // run of consecutive planes: one launch per direction (planes are one allocation)
         while (p + np < 4 && (plane_mask & (1 << (p + np)))) ++np;
-        if (ctx->n >= 2048 && ctx->op_four_step) {
-            // A/B (OCEAN_OP_FOUR_STEP=1; round 3's first N >= 2048 operator, 0.47 of peak at 4 x 4096^2
-            // against 0.63 for the default below):
-            // four-step columns (fft2.hip): per chunk of unit-planes, rows -> scratch (the fused
-            // intermediate's room), C1 on the scratch, C2 scratch -> planes; a chunk of at most
-            // OCEAN_OP_CHUNK_MIB stays in the Infinity Cache between the three launches
-            const int ups = np * (int)ctx->units();
-            const size_t scratch_ups = ctx->inter_units * ctx->P;
-            // auto: 128 MiB, one 4096^2 unit-plane (two: 2.80 against 2.19 ms for 4 x 4096^2 x 4 planes)
-            const long mib = ctx->op_chunk_mib > 0 ? ctx->op_chunk_mib : 128;
-            int k = (int)std::max<size_t>(1, ((size_t)mib << 20) / (up_elems * 8));
-            k = (int)std::min<size_t>((size_t)k, scratch_ups);
-            for (int c0 = 0; c0 < ups; c0 += k) {
-                const int kc = std::min(k, ups - c0);
-                float2* planes = ctx->plane[p] + (size_t)c0 * up_elems;
-                if (int r = timed(ctx, 0, [&] {
-                        return ocean::launch_ifft_four_step(v, planes, kc, ctx->tplane, 0, ctx->stream);
-                    }, "ifft_rows"))
-                    return r;
-                if (int r = timed(ctx, 1, [&] {
-                        hipError_t e = ocean::launch_ifft_four_step(v, planes, kc, ctx->tplane, 1, ctx->stream);
-                        return e != hipSuccess ? e : ocean::launch_ifft_four_step(v, planes, kc, ctx->tplane, 2, ctx->stream);
-                    }, "ifft_cols"))
-                    return r;
-            }
-            p += np;
-            continue;
-        }
-        if (ctx->n >= 2048 && (ctx->op_fold > 0 || (ctx->op_fold < 0 && ctx->n == 4096))) {
+        if (ctx->n == 4096) {
             // Folded columns (fft2.hip k_rowsf / k_colsf): per chunk of unit-planes, rows + the
-            // decimation-in-frequency fold planes -> scratch sub-planes, then 1024-point column tiles
-            // scratch -> planes; a chunk of at most OCEAN_OP_CHUNK_MIB stays in the Infinity
-            // Cache between the two launches (auto 128 MiB: both launches are out of place, so a chunk
-            // occupies twice its size; 4 x 4096^2 x 4 planes, columns 256 / 128 / 64 MiB: 0.44 / 0.71 / 0.71)
+            // decimation-in-frequency fold -> scratch sub-planes, then 2048-point column tiles
+            // scratch -> planes; a chunk of at most OCEAN_OP_CHUNK_MIB stays in the Infinity Cache
+            // between the two launches (auto 128 MiB, one unit-plane: both launches are out of place, so
+            // a chunk occupies twice its size; 4 x 4096^2 x 4 planes, columns 256 / 128 MiB: 0.44 / 0.71)
             const int ups = np * (int)ctx->units();
             const size_t scratch_ups = ctx->inter_units * ctx->P;
-            const long mib = ctx->op_chunk_mib > 0 ? ctx->op_chunk_mib : 128;
+            const long mib = ctx->opt.op_chunk_mib > 0 ? ctx->opt.op_chunk_mib : 128;
             int k = (int)std::max<size_t>(1, ((size_t)mib << 20) / (up_elems * 8));
             k = (int)std::min<size_t>((size_t)k, scratch_ups);
             for (int c0 = 0; c0 < ups; c0 += k) {
                 const int kc = std::min(k, ups - c0);
                 float2* planes = ctx->plane[p] + (size_t)c0 * up_elems;
-                const int fold = ctx->n == 2048 ? 2 : ctx->op_fold_f;
-                if (int r = timed(ctx, 0, [&] {
-                        return ocean::launch_ifft_fold(v, planes, kc, ctx->tplane, 0, fold, ctx->stream);
-                    }, "ifft_rows"))
+                if (int r = timed(ctx, 0, [&] { return ocean::launch_ifft_fold(v, planes, kc, ctx->tplane, 0, ctx->stream); },
+                                  "ifft_rows"))
                     return r;
-                if (int r = timed(ctx, 1, [&] {
-                        const int part = ctx->op_fold_cols == 16 && fold == 4 ? 2 : 1;
-                        return ocean::launch_ifft_fold(v, planes, kc, ctx->tplane, part, fold, ctx->stream);
-                    }, "ifft_cols"))
+                if (int r = timed(ctx, 1, [&] { return ocean::launch_ifft_fold(v, planes, kc, ctx->tplane, 1, ctx->stream); },
+                                  "ifft_cols"))
                     return r;
             }
             p += np;
@@ -714,10 +662,10 @@ int ocean_ifft2d(ocean_ctx* ctx, int plane_mask) {
         // the column launch re-reads the rows' output from the Infinity Cache when the plane set is
         // larger than it.  Auto: 256 MiB (4 x 4 x 1024^2 x 4 planes, 512 MiB, fresh data: 128 / 192 /
         // 256 / 320 / 384 MiB / unchunked 0.69 / 0.69 / 0.736 / 0.63 / 0.60 / 0.57 of peak; cfg3's 128
-        // MiB: one chunk; 4096^2 x 4 planes: 128 / 256 / 512 MiB 0.59 / 0.63 / 0.44).  At N >= 2048 the
-        // column launch takes XCD-grouped pieces of 16-column tiles (fft2.hip Cols2).
+        // MiB: one chunk).  At N = 1024 / 2048 the column launch takes XCD-paired halves of 16-column
+        // tiles (fft2.hip Cols2).
         const int ups = np * (int)ctx->units();
-        const long mib = ctx->op_chunk_mib > 0 ? ctx->op_chunk_mib : 256;
+        const long mib = ctx->opt.op_chunk_mib > 0 ? ctx->opt.op_chunk_mib : 256;
         const int k = (int)std::max<size_t>(1, ((size_t)mib << 20) / (up_elems * 8));
         for (int c0 = 0; c0 < ups; c0 += k) {
             const int kc = std::min(k, ups - c0);
@@ -742,76 +690,6 @@ namespace {
 int step_fused(ocean_ctx* ctx, float time);
 bool use_q(const ocean_ctx* ctx);
 
-void drop_graph(ocean_ctx* ctx) {
-    if (ctx->fg.exec) (void)hipGraphExecDestroy(ctx->fg.exec);
-    if (ctx->fg.g) (void)hipGraphDestroy(ctx->fg.g);
-    ctx->fg = ocean_ctx::FrameGraph{};
-}
-
-// The fused frame as one hipGraph (OCEAN_GRAPH=1): captured from step_fused on the first frame (and
-// again when the schedule changes: column band / parity, three-plane or four-plane), then replayed
-// with the time argument (argument 1 of every pass-A kernel) set on its kernel nodes per frame.
-int step_graph(ocean_ctx* ctx, float time) {
-    auto& fg = ctx->fg;
-    const bool q = use_q(ctx);
-    if (!fg.exec || ctx->graph_stale || fg.x0 != ctx->band_x0 || fg.nx != ctx->band_nx || fg.par != ctx->col_par ||
-        fg.q != q) {
-        drop_graph(ctx);
-        ctx->graph_stale = false;
-        ctx->captured_time_kernels.clear();
-        OCEAN_HIP(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
-        ctx->capturing = true;
-        const int r = step_fused(ctx, time);
-        ctx->capturing = false;
-        hipGraph_t g = nullptr;
-        const hipError_t ec = hipStreamEndCapture(ctx->stream, &g);
-        if (r != OCEAN_OK) {
-            if (g) (void)hipGraphDestroy(g);
-            return r;
-        }
-        if (ec != hipSuccess) return hip_fail(ec, "hipStreamEndCapture");
-        fg.g = g;
-        OCEAN_HIP(hipGraphInstantiate(&fg.exec, g, nullptr, nullptr, 0));
-        size_t n = 0;
-        OCEAN_HIP(hipGraphGetNodes(g, nullptr, &n));
-        std::vector<hipGraphNode_t> nodes(n);
-        OCEAN_HIP(hipGraphGetNodes(g, nodes.data(), &n));
-        for (hipGraphNode_t nd : nodes) {
-            hipGraphNodeType t;
-            OCEAN_HIP(hipGraphNodeGetType(nd, &t));
-            if (t != hipGraphNodeTypeKernel) continue;
-            hipKernelNodeParams p{};
-            OCEAN_HIP(hipGraphKernelNodeGetParams(nd, &p));
-            for (const auto& k : ctx->captured_time_kernels)
-                if (k.first == p.func) {
-                    if (!p.kernelParams || *static_cast<const float*>(p.kernelParams[1]) != time) {
-                        drop_graph(ctx);
-                        return fail(OCEAN_E_DEVICE, "captured frame graph: the pass-A time argument was not found");
-                    }
-                    fg.tnodes.emplace_back(nd, k.second);
-                    break;
-                }
-        }
-        fg.x0 = ctx->band_x0;
-        fg.nx = ctx->band_nx;
-        fg.par = ctx->col_par;
-        fg.q = q;
-    } else {
-        for (const auto& tn : fg.tnodes) {
-            hipKernelNodeParams p{};
-            OCEAN_HIP(hipGraphKernelNodeGetParams(tn.first, &p));
-            void* args[8];
-            for (int i = 0; i < tn.second && i < 8; ++i) args[i] = p.kernelParams[i];
-            float t = time;
-            args[1] = &t;
-            p.kernelParams = args;
-            OCEAN_HIP(hipGraphExecKernelNodeSetParams(fg.exec, tn.first, &p));
-        }
-    }
-    OCEAN_HIP(hipGraphLaunch(fg.exec, ctx->stream));
-    return OCEAN_OK;
-}
-
 // GenerateMips (WaterBody.cs:191-192) when the context has mip chains.
 int generate_mips(ocean_ctx* ctx) {
     if (!(ctx->flags & OCEAN_F_MIPS)) return OCEAN_OK;
@@ -827,10 +705,6 @@ int ocean_step(ocean_ctx* ctx, float time) {
         if (int r = ocean_evolve(ctx, time)) return r;
         if (int r = ocean_ifft2d(ctx, (1 << ctx->P) - 1)) return r;
         if (int r = ocean_fill(ctx)) return r;
-        return generate_mips(ctx);
-    }
-    if (ctx->graph_mode && !ctx->timing) {
-        if (int r = step_graph(ctx, time)) return r;
         return generate_mips(ctx);
     }
     if (int r = step_fused(ctx, time)) return r;
@@ -861,17 +735,17 @@ ocean::DevView sub_view(const ocean::DevView& v, int u0, int nu, bool inter_at_b
 
 // Units per chunk: a frame over many units runs pass A and pass B chunk by chunk so
 // that the intermediate pass B re-reads is still in the 256 MiB Infinity Cache
-// (OCEAN_CHUNK_MIB of intermediate per chunk, 0 = whole frame at once).  Measured on
-// cfg4's 1024 units at 512^2 (8 MiB each): 64 MiB 37.9k, 128 MiB 40.7k, 192 MiB 43.1k,
-// 256 MiB 38.4k, unchunked 40.7k tile-frames/s.
+// (OCEAN_CHUNK_MIB of intermediate per chunk, 0 = whole frame at once; a unit larger than a
+// chunk: whole frame).  Measured on cfg4's 1024 units at 512^2 (8 MiB each): 64 MiB 37.9k,
+// 128 MiB 40.7k, 192 MiB 43.1k, 256 MiB 38.4k, unchunked 40.7k tile-frames/s.
 int chunk_units(const ocean_ctx* ctx, int planes) {
-    const long mib = ctx->chunk_mib;
+    const long mib = ctx->opt.chunk_mib;
     const int U = (int)ctx->units();
     if (mib <= 0) return U;
     const size_t per_unit = ctx->texels() * 8 * planes;
     int k = (int)(((size_t)mib << 20) / per_unit);
     if (k >= ctx->C) k -= k % ctx->C;  // whole tiles when a chunk holds one
-    if (k < 1) k = ctx->chunk_min;
+    if (k < 1) return U;
     return k >= U ? U : k;
 }
 
@@ -881,7 +755,7 @@ int chunk_units(const ocean_ctx* ctx, int planes) {
 // Band widths stay multiples of the four-step tile width (16).
 int c4_bands(const ocean_ctx* ctx, int nx) {
     if (!ocean::pass_c4_supported(ctx->n)) return 1;
-    int nb = ctx->c4_bands;
+    int nb = ctx->opt.c4_bands;
     if (nb <= 0) {
         const size_t band_bytes = (size_t)ctx->P * ctx->n * nx * 8;
         nb = 1;
@@ -894,8 +768,8 @@ int c4_bands(const ocean_ctx* ctx, int nx) {
 // The three-plane fused frame (fftq.hip) runs where it applies: N = 512 / 1024 with full
 // outputs, the mirror-pair row pass's h0k valid.
 bool use_q(const ocean_ctx* ctx) {
-    if (!ctx->q || !ctx->h0_conj || !ocean::pass_q_supported(ctx->n, ctx->P)) return false;
-    return ctx->n >= 2048 || (ctx->a4 && ctx->h0k_valid);  // N <= 1024: the mirror-pair row pass reads h0k
+    if (!ctx->opt.q || !ctx->h0_conj || !ocean::pass_q_supported(ctx->n, ctx->P)) return false;
+    return ctx->n >= 2048 || (ctx->opt.a4 && ctx->h0k_valid);  // N <= 1024: the mirror-pair row pass reads h0k
 }
 
 int step_fused(ocean_ctx* ctx, float time) {
@@ -934,7 +808,7 @@ int step_fused(ocean_ctx* ctx, float time) {
         }
         if (int r = timed(ctx, 0, [&] {
                 // h0k also exists at 4096 (pass A3PP), where the mirror-pair pass A4 does not
-                if (ctx->a4 && ctx->h0k_valid && ocean::pass_a4_supported(ctx->n, ctx->P))
+                if (ctx->opt.a4 && ctx->h0k_valid && ocean::pass_a4_supported(ctx->n, ctx->P))
                     return ocean::launch_pass_a_v4(c, time, ctx->stream);
                 return ocean::launch_pass_a_v3(c, time, ctx->stream);
             }, "pass_a"))
@@ -1088,12 +962,15 @@ int ocean_readback_wait(ocean_readback* rb) {
 
 void ocean_readback_release(ocean_readback* rb) {
     if (!rb) return;
+    int prev = 0;
+    const bool had = hipGetDevice(&prev) == hipSuccess;
     (void)hipSetDevice(rb->device);
     (void)hipEventSynchronize(rb->done);  // the slot is free only once its host copy has landed
     (void)hipEventDestroy(rb->done);
     (void)hipEventDestroy(rb->after);
     rb->pool->give(rb->slot);
     delete rb;
+    if (had) (void)hipSetDevice(prev);  // the caller's current device is left as it was
 }
 
 int ocean_host_alloc(size_t bytes, void** out) {
@@ -1123,7 +1000,6 @@ int ocean_write(ocean_ctx* ctx, int texture, int tile, int cascade, const void* 
     if (texture == OCEAN_TEX_H0) {  // the v3 row pass reads h0 (.zw included); the three-plane frame
         ctx->h0k_valid = false;     // needs .zw = conj h0(-k), which an upload need not keep
         ctx->h0_conj = false;
-        ctx->graph_stale = true;
     }
     if (texture == OCEAN_TEX_TURB) {  // foam state follows the uploaded TURB.x (resume)
         const ocean::DevView v = ctx->view();
@@ -1227,7 +1103,17 @@ int ocean_set_column_parity(ocean_ctx* ctx, int parity) {
     if (ctx->n != 4096) return fail(OCEAN_E_UNSUPPORTED, "a column parity is built for N = 4096 (pass A3P)");
     if (ctx->flags & (OCEAN_F_UNFUSED | OCEAN_F_MIPS | OCEAN_F_DISPLACEMENT_ONLY))
         return fail(OCEAN_E_UNSUPPORTED, "a column parity needs the fused full-output schedule and no mip chains");
-    if (!ctx->q) return fail(OCEAN_E_UNSUPPORTED, "a column parity needs the three-plane frame (OCEAN_Q=0 is set)");
+    if (!ctx->opt.q) return fail(OCEAN_E_UNSUPPORTED, "a column parity needs the three-plane frame (OCEAN_Q=0 is set)");
+    if (!ctx->h0k) {
+        // pass A3PP reads h0(k) of mirror-pair rows from h0k (8 B per texel instead of h0's 16): allocated on
+        // the first parity, then kept up to date by ocean_init_spectrum
+        const size_t bytes = ctx->texels() * ctx->units() * 8;
+        OCEAN_HIP(hipMalloc((void**)&ctx->h0k, bytes));
+        const ocean::DevView v = ctx->view();
+        OCEAN_HIP(ocean::launch_h0k_extract(v, ctx->stream));
+        OCEAN_HIP(hipStreamSynchronize(ctx->stream));
+        ctx->h0k_valid = true;
+    }
     ctx->col_par = parity;
     ctx->band_x0 = 0;
     ctx->band_nx = ctx->n / 2;  // compact: column m of every texture holds x = 2 m + parity
@@ -1262,9 +1148,8 @@ int ocean_step_bytes(ocean_ctx* ctx, uint64_t* pass_a, uint64_t* pass_b) {
         // fill: P planes [+ foam state read + write] -> outputs
         a = tex * (32 + 8 * P + 16 * P);
         b = tex * (16 * P + 8 * P + (full ? 8 : 0) + outs);
-        if (ctx->n >= 2048 && ctx->op_four_step) b += tex * 16 * P;  // four-step columns: C1 and C2
     } else {
-        const bool a4 = ctx->a4 && ctx->h0k_valid && ocean::pass_a4_supported(ctx->n, ctx->P);
+        const bool a4 = ctx->opt.a4 && ctx->h0k_valid && ocean::pass_a4_supported(ctx->n, ctx->P);
         // column band: h0 is read whole (rows are transformed whole), the rest scales with the band
         const uint64_t bt = tex / ctx->n * ctx->band_nx;
         if (use_q(ctx)) {
@@ -1272,7 +1157,7 @@ int ocean_step_bytes(ocean_ctx* ctx, uint64_t* pass_a, uint64_t* pass_b) {
             // N >= 2048) -> Q1..Q3; pass B Q1..Q3 + foam state -> outputs, or at N >= 2048 the
             // four-step passes: C1 reads Q1..Q3 and writes them with R[Q4], C2 reads four planes
             // the column-parity row pass on mirror-pair rows (pass A3PP) reads h0k, 8 B per texel
-            const bool h0k_pairs = ctx->col_par >= 0 && ctx->h0k && ctx->h0k_valid && ocean::pass_a3p_pair_mode();
+            const bool h0k_pairs = ctx->col_par >= 0;
             *pass_a = tex * ((ctx->n >= 2048 && !h0k_pairs) ? 16 : 8) + bt * 24;
             *pass_b = ctx->n >= 2048 ? bt * (24 + 32 + 32 + 8 + outs) : bt * (24 + 8 + outs);
             return OCEAN_OK;

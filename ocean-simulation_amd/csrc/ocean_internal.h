@@ -20,15 +20,12 @@ struct LaunchEvents {
     bool launched;
 };
 LaunchEvents*& launch_events();  // thread-local slot, ocean_abi.cpp
-// Host pointer and argument count of the kernel this thread launched last (ocean_kernel_name reports
-// its symbol; the captured frame graph finds its time argument by it).
+// Host pointer of the kernel this thread launched last (ocean_kernel_name reports its symbol).
 const void*& last_kernel();  // thread-local slot, ocean_abi.cpp
-int& last_kernel_nargs();
 
 template <class F, class... Args>
 inline void launch(F kernel, dim3 grid, dim3 block, uint32_t shmem, hipStream_t s, Args... args) {
     last_kernel() = (const void*)kernel;
-    last_kernel_nargs() = (int)sizeof...(Args);
     LaunchEvents* e = launch_events();
     hipExtLaunchKernelGGL(kernel, grid, block, shmem, s, e && !e->launched ? e->start : nullptr,
                           e ? e->stop : nullptr, 0, args...);
@@ -100,6 +97,8 @@ hipError_t launch_evolve(const DevView& v, float t, hipStream_t s);
 hipError_t launch_fill(const DevView& v, hipStream_t s);
 hipError_t launch_foam_import(const DevView& v, hipStream_t s);
 hipError_t launch_noise(const DevView& v, uint64_t seed, hipStream_t s);
+// h0k = h0.xy (a context whose h0k is allocated after its spectrum: ocean_set_column_parity)
+hipError_t launch_h0k_extract(const DevView& v, hipStream_t s);
 
 // fft2.hip: the operator IFFT (IFFT.InverseFastFourierTransform): persistent,
 // software-pipelined row and column(+permute) launches, in place.
@@ -109,16 +108,11 @@ size_t stage_twiddle_entries(int n);
 // p * U + u of the one plane allocation), in place.
 hipError_t launch_ifft_rows_v2(const DevView& v, float2* base, int ups, hipStream_t s);
 hipError_t launch_ifft_cols_v2(const DevView& v, float2* base, int ups, hipStream_t s);
-// N = 2048 / 4096: the operator over `ups` consecutive unit-planes at `planes` (plane p of unit u is
-// unit-plane p * U + u) through `scratch`; part 0 = rows (planes -> scratch), 1 = four-step column
-// step 1 (in place on scratch), 2 = step 2 + permute (scratch -> planes).
-hipError_t launch_ifft_four_step(const DevView& v, float2* planes, int ups, float2* scratch, int part, hipStream_t s);
-// N = 2048 / 4096: the operator's column transform split by decimation in frequency into `fold` (2 or 4)
-// column transforms of N / fold points (fft2.hip k_rowsf / k_colsf); part 0 = rows + fold (planes ->
-// scratch sub-planes), 1 = the column transforms + permute (scratch -> planes) on XCD-paired 8-column
-// tiles, 2 = the same on 16-column tiles (A/B; fold 4 at 4096, or 2 at 2048).
-hipError_t launch_ifft_fold(const DevView& v, float2* planes, int ups, float2* scratch, int part, int fold,
-                            hipStream_t s);
+// N = 4096: the operator over `ups` consecutive unit-planes at `planes` (plane p of unit u is
+// unit-plane p * U + u) with its column transform split by decimation in frequency into two 2048-point
+// column transforms (fft2.hip k_rowsf / k_colsf); part 0 = rows + fold (planes -> scratch sub-planes),
+// 1 = the column transforms + permute (scratch -> planes) on XCD-paired 8-column tiles.
+hipError_t launch_ifft_fold(const DevView& v, float2* planes, int ups, float2* scratch, int part, hipStream_t s);
 
 // fft3.hip: fused frame through the tile-major intermediate; the row pass
 // recomputes wave data and feeds evolve straight into a radix-4/8 first stage;
@@ -142,7 +136,6 @@ hipError_t launch_pass_a_v4(const DevView& v, float t, hipStream_t s);
 // (mirror-pair rows, N = 512 / 1024) or A3Q (one row per item, N = 2048 / 4096), then pass BQ
 // (column tiles, four transforms, N <= 1024) or the four-step column passes with Q planes.
 bool pass_q_supported(int n, int planes);
-int pass_a3p_pair_mode();  // fftq.hip: row pass of a column-parity shard (0: pass A3P)
 hipError_t launch_pass_a_q(const DevView& v, float t, hipStream_t s);
 hipError_t launch_pass_b_q(const DevView& v, hipStream_t s);
 // fft4k.hip with the three-plane intermediate: C1 also forms and transforms R[Q4] into the fourth

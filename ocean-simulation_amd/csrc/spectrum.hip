@@ -200,6 +200,13 @@ __global__ __launch_bounds__(256) void k_noise(float2* __restrict__ noise, int n
     }
 }
 
+// h0k <- h0.xy (ocean_set_column_parity allocates h0k for pass A3PP after the spectrum may exist)
+__global__ __launch_bounds__(256) void k_h0k_extract(DevView v) {
+    const size_t total = (size_t)v.n * v.n * v.units;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x)
+        v.h0k[i] = *reinterpret_cast<const float2*>(&v.h0[i]);
+}
+
 unsigned grid_for(size_t total) {
     size_t g = (total + 255) / 256;
     return (unsigned)(g < 16384 ? (g == 0 ? 1 : g) : 16384);
@@ -231,6 +238,12 @@ hipError_t launch_evolve(const DevView& v, float t, hipStream_t s) {
 
 hipError_t launch_foam_import(const DevView& v, hipStream_t s) {
     launch(k_foam_import, dim3(grid_for((size_t)v.n * v.n * v.units)), dim3(256), 0, s, v);
+    return hipGetLastError();
+}
+
+hipError_t launch_h0k_extract(const DevView& v, hipStream_t s) {
+    if (!v.h0k) return hipErrorInvalidValue;
+    launch(k_h0k_extract, dim3(grid_for((size_t)v.n * v.n * v.units)), dim3(256), 0, s, v);
     return hipGetLastError();
 }
 

@@ -97,3 +97,22 @@ def test_cpp_host_builds_and_checks_arguments():
     assert os.path.exists(host), "build it: make -C ocean-simulation_amd"
     r = subprocess.run([host], capture_output=True, text=True, timeout=60)
     assert r.returncode == 2 and "usage" in r.stderr
+
+
+def test_env_knobs_match_integration_table():
+    """Every environment variable the library reads (getenv in csrc/) is one of INTEGRATION.md's
+    knob table, and every row of that table is read: no hidden schedule switches, and no knob that
+    skips work."""
+    csrc = os.path.join(ROOT, "ocean-simulation_amd", "csrc")
+    read = set()
+    for name in os.listdir(csrc):
+        src = open(os.path.join(csrc, name)).read()
+        read |= set(re.findall(r'getenv\("([A-Z0-9_]+)"\)', src))
+        assert not re.search(r"getenv\([^\"]", src), f"{name}: getenv of a computed name"
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    sec = text.split("## Environment knobs", 1)[1].split("\n## ", 1)[0]
+    table = set(re.findall(r"^\| `([A-Z0-9_]+)`", sec, flags=re.M))
+    assert read == table, f"read but undocumented: {read - table}; documented but not read: {table - read}"
+    strings = open(oh.LIB_PATH, "rb").read()
+    for word in (b"NOSTORE", b"A3_VARIANT", b"A4_WHOLE", b"OCEAN_GRAPH"):
+        assert word not in strings, word

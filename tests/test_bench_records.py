@@ -1,6 +1,8 @@
 """Host logic of bench.py's profile lookups (no GPU): roofline.traffic and the rocprofv3 figures are
-taken only from records of the exact kernel symbol that ran, and the builder's
-micro-benchmark ceilings only from this round's profiles/<ROUND>* directories."""
+taken only from stamped records of the exact kernel symbol that ran and of the same config, preferring
+the record made with the loaded library (then with its sources, then the newest stamp), never by
+directory name; the builder's micro-benchmark ceilings only from this round's
+profiles/<ROUND>* directories, ROUND derived from the driver's BENCH records."""
 import json
 import os
 import sys
@@ -22,33 +24,51 @@ SYM_BQ = "void ocean::(anonymous namespace)::k_pass_bq<1024, false, 0>(ocean::De
 SYM_B3 = "void ocean::(anonymous namespace)::k_pass_b3<1024, false, 0>(ocean::DevView, int)"
 
 
-def _pmc(d, config, kernels):
+def _rec(d, config, kernels, lib="L0", src="S0", utc="2026-01-01T00:00:00Z", stamp=True):
+    """kernels: {symbol: (avg_ns, hbm_bytes_per_launch)}"""
     os.makedirs(d, exist_ok=True)
-    json.dump({"config": config, "kernels": {k: {"hbm_bytes_per_launch": v} for k, v in kernels.items()}},
-              open(os.path.join(d, "pmc_summary.json"), "w"))
-
-
-def test_pmc_traffic_exact_symbol_and_config(bench, tmp_path):
-    _pmc(tmp_path / "r02a", "cfg3", {SYM_B3: 111, SYM_BQ: 222})
-    _pmc(tmp_path / "r03a", "cfg3", {SYM_B3: 333})       # newer, but only the stale kernel
-    _pmc(tmp_path / "r03b", "cfg4", {SYM_BQ: 444})       # the kernel, but another config
-    assert bench.pmc_traffic(SYM_BQ, "cfg3", str(tmp_path)) == (222, "r02a")
-    assert bench.pmc_traffic(SYM_BQ, "cfg4", str(tmp_path)) == (444, "r03b")
-    assert bench.pmc_traffic(SYM_B3.replace("1024", "512"), "cfg3", str(tmp_path)) is None
-    # a substring of the symbol is not a match
-    assert bench.pmc_traffic("k_pass_bq", "cfg3", str(tmp_path)) is None
-    assert bench.pmc_traffic(None, "cfg3", str(tmp_path)) is None
-
-
-def test_rocprof_kernel_us_exact_symbol(bench, tmp_path):
-    d = tmp_path / "r03x"
-    os.makedirs(d)
-    with open(d / "ifft_kernel_stats.csv", "w") as f:
+    with open(os.path.join(d, "kernel_stats.csv"), "w") as f:
         f.write('"Name","Calls","TotalDurationNs","AverageNs"\n')
-        f.write(f'"{SYM_B3}",10,1000,100.0\n"{SYM_BQ}",10,5000,500.0\n')
-    assert bench.rocprof_kernel_us("ifft_kernel_stats.csv", SYM_BQ, str(tmp_path)) == (
-        0.5, "profiles/r03x/ifft_kernel_stats.csv")
-    assert bench.rocprof_kernel_us("ifft_kernel_stats.csv", "k_pass", str(tmp_path)) is None
+        for k, (ns, _) in kernels.items():
+            f.write(f'"{k}",10,{10 * ns},{ns}\n')
+    json.dump({"config": config, "kernels": {k: {"hbm_bytes_per_launch": b} for k, (_, b) in kernels.items()}},
+              open(os.path.join(d, "pmc_summary.json"), "w"))
+    if stamp:
+        json.dump({"config": config, "lib_sha256": lib, "src_sha256": src, "utc": utc},
+                  open(os.path.join(d, "stamp.json"), "w"))
+
+
+def test_record_exact_symbol_config_and_stamp(bench, tmp_path, monkeypatch):
+    monkeypatch.setattr(bench, "_IDENT", {"lib": "LIB", "src": "SRC"})
+    _rec(tmp_path / "zz_old", "cfg3", {SYM_BQ: (500.0, 222)}, utc="2026-01-01T00:00:00Z")
+    _rec(tmp_path / "aa_new", "cfg3", {SYM_BQ: (400.0, 333)}, utc="2026-02-01T00:00:00Z")
+    # newest stamp wins when no stamp matches the library (not the alphabetically last directory)
+    r = bench.find_record("cfg3", SYM_BQ, str(tmp_path))
+    assert (r["traffic_bytes_per_launch"], r["dir"], r["match"]) == (333, "profiles/aa_new", "none")
+    assert r["avg_us"] == 0.4
+    # a record of the same sources beats a newer one; one of the same library beats both
+    _rec(tmp_path / "mm_src", "cfg3", {SYM_BQ: (450.0, 444)}, src="SRC", utc="2025-12-01T00:00:00Z")
+    assert bench.find_record("cfg3", SYM_BQ, str(tmp_path))["match"] == "src"
+    _rec(tmp_path / "bb_lib", "cfg3", {SYM_BQ: (420.0, 555)}, lib="LIB", utc="2025-11-01T00:00:00Z")
+    r = bench.find_record("cfg3", SYM_BQ, str(tmp_path))
+    assert (r["traffic_bytes_per_launch"], r["match"]) == (555, "lib")
+    # another config, another symbol, a substring, no symbol, an unstamped directory: no record
+    _rec(tmp_path / "cc_cfg4", "cfg4", {SYM_BQ: (900.0, 666)}, lib="LIB", utc="2027-01-01T00:00:00Z")
+    assert bench.find_record("cfg3", SYM_BQ, str(tmp_path))["traffic_bytes_per_launch"] == 555
+    assert bench.find_record("cfg4", SYM_BQ, str(tmp_path))["traffic_bytes_per_launch"] == 666
+    assert bench.find_record("cfg3", SYM_B3, str(tmp_path)) is None
+    assert bench.find_record("cfg3", "k_pass_bq", str(tmp_path)) is None
+    assert bench.find_record("cfg3", None, str(tmp_path)) is None
+    _rec(tmp_path / "dd_unstamped", "cfg3", {SYM_B3: (100.0, 1)}, stamp=False)
+    assert bench.find_record("cfg3", SYM_B3, str(tmp_path)) is None
+
+
+def test_round_is_derived(bench, tmp_path):
+    assert bench._current_round(str(tmp_path)) == "r01"
+    (tmp_path / "BENCH_r01.json").write_text("{}")
+    (tmp_path / "BENCH_r03.json").write_text("{}")
+    assert bench._current_round(str(tmp_path)) == "r04"
+    assert bench.ROUND == bench._current_round(ROOT)
 
 
 def test_ceilings_only_from_this_round(bench, tmp_path):

@@ -102,33 +102,12 @@ def test_ifft2d_operator_vs_oracle(n):
     ctx.close()
 
 
-# operator schedules at N >= 2048 (ocean_ifft2d, ocean_abi.cpp): the default (folded columns at 4096,
-# XCD-grouped whole-column tiles at 2048), and the A/B knobs, read at ocean_create
-OP_MODES = {
-    "default": {},
-    "fold": {"OCEAN_OP_FOLD": "1"},                            # folded columns at 2048 too
-    "fold16": {"OCEAN_OP_FOLD": "1", "OCEAN_FOLD_COLS": "16"},  # folded columns on 16-column tiles
-    "grouped": {"OCEAN_OP_FOLD": "0"},                         # whole-column tiles grouped on one XCD
-    "fold2": {"OCEAN_FOLD_F": "2"},                            # at 4096: two rows folded, 2048-point columns
-    "fold4": {"OCEAN_FOLD_F": "4"},                            # at 4096: four rows folded, 1024-point columns
-    "four_step": {"OCEAN_OP_FOUR_STEP": "1"},
-}
-
-
-@pytest.mark.parametrize("n,C,mask,mode", [(2048, 1, 0b0001, "default"), (4096, 4, 0b1111, "default"),
-                                           (2048, 1, 0b0001, "fold"), (4096, 1, 0b0110, "fold16"),
-                                           (4096, 4, 0b1111, "grouped"), (4096, 2, 0b1001, "fold2"),
-                                           (4096, 2, 0b1001, "fold4"),
-                                           (2048, 1, 0b0001, "four_step"),
-                                           (4096, 4, 0b1111, "four_step")])
-def test_ifft2d_operator_large_vs_numpy(n, C, mask, mode, monkeypatch):
+@pytest.mark.parametrize("n,C,mask", [(2048, 1, 0b0001), (4096, 4, 0b1111), (4096, 1, 0b0110), (4096, 2, 0b1001)])
+def test_ifft2d_operator_large_vs_numpy(n, C, mask):
     """The operator at N = 2048 / 4096 on every requested plane of every cascade, against numpy's
-    float64 ifft2 (ref64); 4 x 4096^2 x 4 planes is cfg5's whole plane set (2 GiB).  Default at 4096:
-    rows + decimation-in-frequency fold into the scratch, then 1024-point column tiles (fft2.hip
-    k_rowsf / k_colsf); at 2048 in-place rows, then whole-column tiles grouped on one XCD (Cols2); the
-    other OP_MODES are the A/B schedules."""
-    for k, val in OP_MODES[mode].items():
-        monkeypatch.setenv(k, val)
+    float64 ifft2 (ref64); 4 x 4096^2 x 4 planes is cfg5's whole plane set (2 GiB).  At 4096: rows +
+    decimation-in-frequency fold into the scratch, then 2048-point column tiles (fft2.hip k_rowsf /
+    k_colsf); at 2048 in-place rows, then XCD-paired 8-column halves of whole columns (Cols2)."""
     ctx = oh.OceanContext(n, C, 1)
     planes = [p for p in range(4) if mask >> p & 1]
 
@@ -152,30 +131,31 @@ def test_ifft2d_operator_large_vs_numpy(n, C, mask, mode, monkeypatch):
     ctx.close()
 
 
-@pytest.mark.parametrize("chunk_mib,mode", [(None, "default"), (64, "default"), (None, "four_step"),
-                                            (64, "four_step"), (None, "fold"), (64, "fold"), (32, "fold16")])
-def test_ifft2d_operator_2048_vs_oracle(chunk_mib, mode, monkeypatch):
-    """N = 2048 operator against the reference's radix-2 schedule (oracle) on three planes of two
-    cascades (6 unit-planes of 32 MiB): one chunk by default, or 3 / 6 chunks at OCEAN_OP_CHUNK_MIB=64 /
-    32; plane 3 untouched; every OP_MODES schedule."""
+@pytest.mark.parametrize("n,chunk_mib", [(2048, None), (2048, 64), (4096, None), (4096, 256)])
+def test_ifft2d_operator_large_vs_oracle(n, chunk_mib, monkeypatch):
+    """N = 2048 / 4096 operator against the reference's radix-2 schedule (oracle) on three planes of two
+    cascades (6 unit-planes): one chunk per unit-plane at 4096 by default (two at OCEAN_OP_CHUNK_MIB=256),
+    one chunk at 2048 by default (three at 64); plane 3 untouched."""
     if chunk_mib:
         monkeypatch.setenv("OCEAN_OP_CHUNK_MIB", str(chunk_mib))
-    for k, val in OP_MODES[mode].items():
-        monkeypatch.setenv(k, val)
-    n, C = 2048, 2
-    ctx = oh.OceanContext(n, C, 1)
-    rng = np.random.default_rng(7)
-    planes = [rng.standard_normal((C, n, n, 2)).astype(np.float32) for _ in range(4)]
-    for p in range(4):
-        for c in range(C):
-            ctx.write(oh.TEX_PLANE0 + p, planes[p][c], 0, c)
-    ctx.ifft2d(0b0111)
-    np.testing.assert_array_equal(ctx.read_all(oh.TEX_PLANE3), planes[3])
-    for p in range(3):
-        got = ctx.read_all(oh.TEX_PLANE0 + p)
-        want = O.ifft2d(planes[p])
-        for c in range(C):
-            assert O.rel_err(cplx(got[c]), cplx(want[c])) <= TOL, f"plane {p} cascade {c}"
+    C = 2
+    O.set_threads(oracle_threads())
+    try:
+        ctx = oh.OceanContext(n, C, 1)
+        rng = np.random.default_rng(7)
+        planes = [rng.standard_normal((C, n, n, 2)).astype(np.float32) for _ in range(4)]
+        for p in range(4):
+            for c in range(C):
+                ctx.write(oh.TEX_PLANE0 + p, planes[p][c], 0, c)
+        ctx.ifft2d(0b0111)
+        np.testing.assert_array_equal(ctx.read_all(oh.TEX_PLANE3), planes[3])
+        for p in range(3):
+            got = ctx.read_all(oh.TEX_PLANE0 + p)
+            want = O.ifft2d(planes[p])
+            for c in range(C):
+                assert O.rel_err(cplx(got[c]), cplx(want[c])) <= TOL, f"plane {p} cascade {c}"
+    finally:
+        O.set_threads(1)
     ctx.close()
 
 
@@ -255,12 +235,14 @@ def oracle_threads():
     return int(os.environ.get("OMP_NUM_THREADS") or min(16, os.cpu_count() or 1))
 
 
-@pytest.mark.parametrize("n,ncasc,flags", [(256, 1, 0), (512, 1, oh.F_DISPLACEMENT_ONLY), (512, 3, 0),
+@pytest.mark.parametrize("n,ncasc,flags", [(256, 1, 0), (256, 2, oh.F_DISPLACEMENT_ONLY),
+                                           (512, 1, oh.F_DISPLACEMENT_ONLY), (512, 3, 0),
                                            (1024, 4, 0), (1024, 4, oh.F_UNFUSED), (2048, 1, 0),
                                            (2048, 1, oh.F_UNFUSED), (4096, 1, 0), (4096, 1, oh.F_UNFUSED),
                                            (4096, 1, oh.F_DISPLACEMENT_ONLY), (4096, 4, 0)])
 def test_frames_vs_oracle(n, ncasc, flags):
-    """BASELINE configs: cfg1-shaped 256^2 x1, cfg2 512^2 displacement only, the scene (512^2 x3),
+    """BASELINE configs: cfg1-shaped 256^2 x1, cfg2 512^2 displacement only (pass A8 + B8; 256^2: the
+    two-plane pass A4 + the side-by-side pass B2D), the scene (512^2 x3),
     cfg3 4 x 1024^2 full outputs, one cfg5 cascade at 4096^2 and cfg5 whole (4 x 4096^2: a 2 GiB
     plane array, 2^31 bytes) through the four-step column passes, against the radix-2 oracle at
     full size; 3 frames (2 for cfg5 whole) so the foam state is exercised.  F_UNFUSED at 2048 / 4096:
@@ -744,6 +726,36 @@ def test_device_noise_matches_restatement():
     ctx.close()
 
 
+def test_whole_frame_intermediate_past_4gib():
+    """OCEAN_CHUNK_MIB=0 (one chunk over every unit) on 43 tiles x 4 cascades x 1024^2: the three-plane
+    intermediate is 172 units x 24 MiB > 4 GiB, past the 32-bit store offsets of pass AQ, which then
+    takes its 64-bit form (fftq.hip go_aq).  Tiles 0 and 42 equal single-tile contexts (the
+    32-bit form) bit for bit over two frames."""
+    n, cas, T, seed = 1024, O.SCENE_CASCADES, 43, 20251121
+    os.environ["OCEAN_CHUNK_MIB"] = "0"  # read once, in ocean_create
+    try:
+        big = oh.OceanContext(n, 4, T)
+    finally:
+        os.environ.pop("OCEAN_CHUNK_MIB", None)
+    big.set_params(O.scene_params(), cas)
+    big.generate_noise_device(seed)
+    big.init_spectrum()
+    times = (0.5, 1.0)
+    for t in times:
+        big.step(t)
+    for tile in (0, T - 1):
+        single = oh.OceanContext(n, 4, 1)
+        single.set_params(O.scene_params(), cas)
+        single.set_noise(0, big.read(oh.TEX_NOISE, tile))
+        single.init_spectrum()
+        for t in times:
+            single.step(t)
+        for tex in (oh.TEX_DISP, oh.TEX_DERIV, oh.TEX_TURB):
+            np.testing.assert_array_equal(big.read_all(tex, tile), single.read_all(tex), err_msg=f"tile {tile}")
+        single.close()
+    big.close()
+
+
 def test_chunked_frame_equals_whole_frame():
     """Many units: pass A / pass B run per unit chunk (Infinity-Cache-sized); results equal
     the single-launch frame bit for bit."""
@@ -842,54 +854,6 @@ def test_column_parity_shards_vs_oracle():
         ctx.close()
 
 
-_PARITY_SCRIPT = r"""
-import sys, numpy as np
-import ocean_hip as oh
-import oracle as O
-out = sys.argv[1]
-res = []
-for c in (0, 3):
-    for b in (0, 1):
-        ctx = oh.OceanContext(4096, 1, 1)
-        ctx.set_params(O.scene_params(), O.SCENE_CASCADES[c:c + 1])
-        ctx.set_noise(0, O.generate_noise(4096, 20251121))
-        ctx.init_spectrum()
-        ctx.set_column_parity(b)
-        for t in (0.25, 3.0):
-            ctx.step(t)
-        res += [ctx.read(tex)[:, :2048] for tex in (oh.TEX_DISP, oh.TEX_DERIV, oh.TEX_TURB)]
-        ctx.close()
-np.savez(out, *res)
-"""
-
-
-def test_column_parity_row_pass_variants(tmp_path):
-    """The column-parity shard's row pass in its three forms (OCEAN_A3P_PAIR, read once per process):
-    pass A3PP on mirror-pair rows with 1024 lanes (3, the default; 4 loads the next pair after the
-    stages) and 512 lanes (1), and pass A3P
-    on single rows with full h0 (0).  Their radix orders and factor sharing differ, so they agree
-    within the fp32 tolerance, not bit for bit: cascades 0 and 3, both parities, two frames with foam,
-    every channel at 1e-5 norm-relative against the default (which the oracle test above pins)."""
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env_base = dict(os.environ)
-    env_base["PYTHONPATH"] = os.pathsep.join([os.path.join(root, "ocean-simulation_amd"), os.path.join(root, "oracle"),
-                                              env_base.get("PYTHONPATH", "")])
-    res = {}
-    for val in ("3", "4", "1", "0"):
-        out = str(tmp_path / f"pair_{val}.npz")
-        subprocess.run([sys.executable, "-c", _PARITY_SCRIPT, out], env=dict(env_base, OCEAN_A3P_PAIR=val),
-                       check=True, timeout=200)
-        with np.load(out) as z:
-            res[val] = [z[k] for k in sorted(z.files, key=lambda k: int(k.split("_")[1]))]
-    for val in ("1", "0"):
-        for i, (a, b) in enumerate(zip(res[val], res["3"])):
-            assert_channels(a[None], b[None], what=f"OCEAN_A3P_PAIR={val} texture {i}")
-    for a, b in zip(res["4"], res["3"]):  # the same arithmetic, only the load moves
-        np.testing.assert_array_equal(a, b)
-
-
 def test_column_parity_errors():
     ctx, _ = make_ctx(1024, O.SCENE_CASCADES[:1])
     with pytest.raises(oh.OceanError) as e:
@@ -967,87 +931,3 @@ def test_four_step_column_bands_bit_identical(n, bands):
         np.testing.assert_array_equal(a.read_all(tex), b.read_all(tex))
     a.close()
     b.close()
-
-
-_VARIANT_SCRIPT = r"""
-import sys, numpy as np
-import ocean_hip as oh
-import oracle as O
-n, ncasc, flags, out = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
-ctx = oh.OceanContext(n, ncasc, 1, flags)
-ctx.set_params(O.scene_params(), O.SCENE_CASCADES[:ncasc])
-ctx.generate_noise(20251121)
-ctx.init_spectrum()
-for t in (0.0, 0.5, 250.0):
-    ctx.step(t)
-texs = (oh.TEX_DISP,) if flags else (oh.TEX_DISP, oh.TEX_DERIV, oh.TEX_TURB)
-np.savez(out, *[ctx.read_all(t) for t in texs])
-ctx.close()
-"""
-
-
-@pytest.mark.parametrize("var,n,ncasc,flags", [("OCEAN_B2D", 512, 1, oh.F_DISPLACEMENT_ONLY),
-                                               ("OCEAN_B2D", 256, 2, oh.F_DISPLACEMENT_ONLY),
-                                               ("OCEAN_A3Q_S3", 4096, 1, 0), ("OCEAN_A3Q_PF", 4096, 1, 0),
-                                               ("OCEAN_A3_EPF", 4096, 1, oh.F_DISPLACEMENT_ONLY),
-                                               ("OCEAN_GRAPH", 512, 1, oh.F_DISPLACEMENT_ONLY),
-                                               ("OCEAN_GRAPH", 1024, 4, 0)])
-def test_launch_variants_bit_identical(tmp_path, var, n, ncasc, flags):
-    """Schedule knobs read once per process at first launch (environment knobs):
-    side-by-side vs sequential pass-B planes (B2D), pass A3Q's idle-slot skip (S3) and early h0
-    prefetch (PF), pass A3's early prefetch at N = 4096 (EPF), the frame replayed as one captured
-    hipGraph with its time argument updated per frame (GRAPH).  Each variant runs in its own
-    process; 3 frames incl. foam, every output bit equal."""
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env_base = dict(os.environ)
-    if var == "OCEAN_B2D":
-        env_base["OCEAN_B8"] = "0"  # pass B8 (the N = 512 default) has no sequential form
-    env_base["PYTHONPATH"] = os.pathsep.join([os.path.join(root, "ocean-simulation_amd"), os.path.join(root, "oracle"),
-                                              env_base.get("PYTHONPATH", "")])
-    res = []
-    for val in ("1", "0"):
-        out = str(tmp_path / f"{var}_{val}.npz")
-        env = dict(env_base, **{var: val})
-        subprocess.run([sys.executable, "-c", _VARIANT_SCRIPT, str(n), str(ncasc), str(flags), out], env=env,
-                       check=True, timeout=100)
-        with np.load(out) as z:
-            res.append([z[k] for k in sorted(z.files)])
-    for a, b in zip(*res):
-        np.testing.assert_array_equal(a, b)
-
-
-@pytest.mark.parametrize("var,val,n,ncasc,flags", [("OCEAN_B8", "0", 512, 1, oh.F_DISPLACEMENT_ONLY),
-                                                   ("OCEAN_B8", "0", 512, 2, oh.F_DISPLACEMENT_ONLY),
-                                                   ("OCEAN_A8", "0", 512, 1, oh.F_DISPLACEMENT_ONLY),
-                                                   ("OCEAN_AQ_ROWS", "3", 1024, 4, 0),
-                                                   ("OCEAN_AQ_ROWS", "2", 1024, 2, 0),
-                                                   ("OCEAN_A3Q_SHARE", "1", 4096, 1, 0)])
-def test_launch_variants_vs_oracle(tmp_path, var, val, n, ncasc, flags):
-    """Variants whose radix order or arithmetic differs from the default's (OCEAN_B8=0: pass B's radix-16
-    engine instead of pass B8's radix 8 x 8 x 8; OCEAN_A8=0: pass A4's radix-16 engine; OCEAN_AQ_ROWS:
-    the one-row three-plane pass at 1024 instead of the mirror-pair one, 2 = slim image, 3 = also the
-    mirror factors exchanged; OCEAN_A3Q_SHARE=1: the exchanged factors at 4096, reciprocal 1/|k|), so
-    they match within the fp32 tolerance, not bit for bit: each runs in its own process (knobs are read once per
-    process), and its third frame (t = 250 s, foam over all three) is checked against the radix-2 oracle at 1e-5 norm-relative per channel and cascade."""
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, **{var: val})
-    env["PYTHONPATH"] = os.pathsep.join([os.path.join(root, "ocean-simulation_amd"), os.path.join(root, "oracle"),
-                                         env.get("PYTHONPATH", "")])
-    out = str(tmp_path / f"{var}_{val}.npz")
-    subprocess.run([sys.executable, "-c", _VARIANT_SCRIPT, str(n), str(ncasc), str(flags), out],
-                   env=env, check=True, timeout=100)
-    cas = O.SCENE_CASCADES[:ncasc]
-    full = not flags & oh.F_DISPLACEMENT_ONLY
-    oc = O.OracleOcean(n, O.scene_params(), cas, O.generate_noise(n, 20251121), nplanes=4 if full else 2)
-    for t in (0.0, 0.5, 250.0):  # the script's frames
-        ref = oc.step(t)
-    with np.load(out) as z:
-        got = [z[k] for k in sorted(z.files)]
-    assert_channels(got[0][..., :3], ref[0][..., :3], what=f"{var}={val} disp")
-    if full:
-        assert_channels(got[1], ref[1], what=f"{var}={val} deriv")
-        assert_channels(got[2], ref[2], what=f"{var}={val} turb")
