@@ -300,6 +300,25 @@ def ifft_beyond_cache(reps=50):
         ctx.close()
 
 
+def mip_record(launches_per_frame, profiles_dir=PROFILES):
+    """The mip kernels' time per frame from the committed rocprofv3 record of the update loop (config
+    "update_loop", tools/profile.sh running `bench.py --only-update-loop`): every k_mips_* kernel of the
+    record chosen by find_record's rule (stamp matching the loaded library first), its average duration
+    weighted by its share of the launches, times the library's mip launches per frame."""
+    import csv
+    names = ("void ocean::(anonymous namespace)::k_mips_block(ocean::DevView, int, int)",
+             "void ocean::(anonymous namespace)::k_mips_tail(ocean::DevView, int)")
+    recs = {nm: find_record("update_loop", nm, profiles_dir) for nm in names}
+    if any(r is None for r in recs.values()) or len({r["dir"] for r in recs.values()}) != 1:
+        return None
+    calls = sum(r["launches"] for r in recs.values())
+    us = sum(r["avg_us"] * r["launches"] for r in recs.values()) / calls * launches_per_frame
+    r0 = next(iter(recs.values()))
+    return {"dir": r0["dir"], "match": r0["match"], "utc": r0["utc"], "us_per_frame": round(us, 2),
+            "kernels": {nm.split("::")[-1].split("(")[0]: {"avg_us": round(r["avg_us"], 3), "launches": r["launches"]}
+                        for nm, r in recs.items()}}
+
+
 def update_loop(steps=200, warmup=20):
     """The reference's per-frame loop at cfg3, as a Unity host over this library runs it
     (WaterBody.Update, WaterBody.cs:284-297): CalculateWavesTexturesAtTime with the mip chains of DERIV
@@ -338,6 +357,7 @@ def update_loop(steps=200, warmup=20):
         wb.WaitForReadback()  # every requested readback has landed inside the timed region
         loop_s = (time.perf_counter() - t0) / steps
         slice_bytes = 1024 * 1024 * 16
+        mips_rec = mip_record(nm / steps)
         return {"workload": "cfg3 (4 x 1024^2) frame + GenerateMips of DERIV and TURB + AsyncGPUReadback of "
                             "DISP slice 0 every frame, ocean_hip.WaterBody.Update (WaterBody.cs:284-297)",
                 "frames_per_s": round(1.0 / loop_s, 2), "ms_per_frame": round(1e3 * loop_s, 4),
@@ -346,7 +366,8 @@ def update_loop(steps=200, warmup=20):
                 "step_with_mips": {"frames_per_s": round(1.0 / step_s, 2), "ms_per_frame": round(1e3 * step_s, 4),
                                    "kernel_us": {"pass_a": round(1e3 * ka / steps, 2), "pass_b": round(1e3 * kb / steps, 2),
                                                  "mips": round(1e3 * km / steps, 2)},
-                                   "mip_launches_per_frame": nm / steps, "mips_symbol_last": mips_sym}}
+                                   "mip_launches_per_frame": nm / steps, "mips_symbol_last": mips_sym,
+                                   "mips_rocprof": mips_rec}}
     finally:
         wb.OnDisable()
 
@@ -412,7 +433,12 @@ def main():
     ap.add_argument("--no-update-loop", action="store_true")
     ap.add_argument("--no-interleave", action="store_true",
                     help="cfg5 past one GPU per cascade: contiguous column bands instead of even / odd columns")
+    ap.add_argument("--only-update-loop", action="store_true",
+                    help="run update_loop alone and print its JSON (the rocprofv3 record of the mip kernels)")
     args = ap.parse_args()
+    if args.only_update_loop:
+        print(json.dumps(update_loop(max(50, args.steps // 2), args.warmup)))
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -10,7 +10,7 @@ for r in $(seq 1 ${4:-2}); do
     lib=ocean-simulation_amd/ocean_hip/liboceanhip.so
     [ "$v" != base ] && lib=ocean-simulation_amd/ocean_hip/liboceanhip_$v.so
     env OCEAN_HIP_LIB=$PWD/$lib $(echo $e | tr ',' ' ') timeout -k 10 300 python bench.py --config $1 --steps ${3:-50} \
-      --warmup 5 --no-cpu-baseline --no-ifft-stage --no-beyond-cache > gpurun_out/abe_$i.json 2> gpurun_out/abe_$i.err
+      --warmup 5 --no-cpu-baseline --no-ifft-stage --no-beyond-cache --no-update-loop > gpurun_out/abe_$i.json 2> gpurun_out/abe_$i.err
     echo "$r $vc $(python -c "import json;d=json.load(open('gpurun_out/abe_$i.json'));print(d['value'],d['kernels_us'])")"
   done
 done
