@@ -306,8 +306,8 @@ def mip_record(launches_per_frame, profiles_dir=PROFILES):
     record chosen by find_record's rule (stamp matching the loaded library first), its average duration
     weighted by its share of the launches, times the library's mip launches per frame."""
     import csv
-    names = ("void ocean::(anonymous namespace)::k_mips_block(ocean::DevView, int, int)",
-             "void ocean::(anonymous namespace)::k_mips_tail(ocean::DevView, int)")
+    names = ("ocean::(anonymous namespace)::k_mips_block(ocean::DevView, int, int)",
+             "ocean::(anonymous namespace)::k_mips_tail(ocean::DevView, int)")
     recs = {nm: find_record("update_loop", nm, profiles_dir) for nm in names}
     if any(r is None for r in recs.values()) or len({r["dir"] for r in recs.values()}) != 1:
         return None
