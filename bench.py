@@ -300,22 +300,24 @@ def ifft_beyond_cache(reps=50):
         ctx.close()
 
 
-def mip_record(launches_per_frame, profiles_dir=PROFILES):
+def mip_record(profiles_dir=PROFILES):
     """The mip kernels' time per frame from the committed rocprofv3 record of the update loop (config
-    "update_loop", tools/profile.sh running `bench.py --only-update-loop`): every k_mips_* kernel of the
-    record chosen by find_record's rule (stamp matching the loaded library first), its average duration
-    weighted by its share of the launches, times the library's mip launches per frame."""
-    import csv
+    "update_loop", tools/profile.sh running `bench.py --only-update-loop`): the k_mips_* kernels of the
+    record chosen by find_record's rule (stamp matching the loaded library first), total duration per
+    frame."""
+    import re
     names = ("ocean::(anonymous namespace)::k_mips_block(ocean::DevView, int, int)",
              "ocean::(anonymous namespace)::k_mips_tail(ocean::DevView, int)")
     recs = {nm: find_record("update_loop", nm, profiles_dir) for nm in names}
     if any(r is None for r in recs.values()) or len({r["dir"] for r in recs.values()}) != 1:
         return None
-    calls = sum(r["launches"] for r in recs.values())
-    us = sum(r["avg_us"] * r["launches"] for r in recs.values()) / calls * launches_per_frame
+    # ocean_step launches k_mips_block once per frame (both chains, every slice), then k_mips_tail when
+    # the chain is deeper than one block's levels (csrc/mips.hip): frames = the block kernel's calls
+    frames = recs[names[0]]["launches"]
+    us = sum(r["avg_us"] * r["launches"] for r in recs.values()) / frames
     r0 = next(iter(recs.values()))
     return {"dir": r0["dir"], "match": r0["match"], "utc": r0["utc"], "us_per_frame": round(us, 2),
-            "kernels": {nm.split("::")[-1].split("(")[0]: {"avg_us": round(r["avg_us"], 3), "launches": r["launches"]}
+            "kernels": {re.search(r"k_\w+", nm).group(0): {"avg_us": round(r["avg_us"], 3), "launches": r["launches"]}
                         for nm, r in recs.items()}}
 
 
@@ -357,7 +359,7 @@ def update_loop(steps=200, warmup=20):
         wb.WaitForReadback()  # every requested readback has landed inside the timed region
         loop_s = (time.perf_counter() - t0) / steps
         slice_bytes = 1024 * 1024 * 16
-        mips_rec = mip_record(nm / steps)
+        mips_rec = mip_record()
         return {"workload": "cfg3 (4 x 1024^2) frame + GenerateMips of DERIV and TURB + AsyncGPUReadback of "
                             "DISP slice 0 every frame, ocean_hip.WaterBody.Update (WaterBody.cs:284-297)",
                 "frames_per_s": round(1.0 / loop_s, 2), "ms_per_frame": round(1e3 * loop_s, 4),

@@ -86,3 +86,17 @@ def test_ceilings_only_from_this_round(bench, tmp_path):
     wc = bench.write_ceilings(str(tmp_path))
     assert wc["nt_192MiB_GBs"] == 4600.0 and wc["nt_beyond_cache_GBs"] == 4069.1
     assert bench.shape_us("aqbench.txt", "AQ rows (y, N - y), half lines", str(tmp_path))[0] == 17.0
+
+
+def test_mip_record_per_frame(bench, tmp_path, monkeypatch):
+    """update_loop's mip kernels from the update_loop record: k_mips_block runs once per frame, so
+    the per-frame time is the record's total mip time over the block kernel's launches."""
+    monkeypatch.setattr(bench, "_IDENT", {"lib": "LIB", "src": "SRC"})
+    blk = "ocean::(anonymous namespace)::k_mips_block(ocean::DevView, int, int)"
+    tail = "ocean::(anonymous namespace)::k_mips_tail(ocean::DevView, int)"
+    assert bench.mip_record(str(tmp_path)) is None
+    _rec(tmp_path / "r04u", "update_loop", {blk: (30000.0, 1), tail: (6000.0, 1)}, lib="LIB")
+    r = bench.mip_record(str(tmp_path))
+    assert r["us_per_frame"] == 36.0 and r["match"] == "lib" and set(r["kernels"]) == {"k_mips_block", "k_mips_tail"}
+    _rec(tmp_path / "r04c", "cfg3", {blk: (1.0, 1), tail: (1.0, 1)}, lib="LIB", utc="2027-01-01T00:00:00Z")
+    assert bench.mip_record(str(tmp_path))["dir"] == "profiles/r04u"  # another config's record never stands in

@@ -6,6 +6,10 @@ set -o pipefail
 OUT=gpurun_out/r04_final; mkdir -p $OUT
 export TMPDIR=/tmp
 bash tools/sessions/r04_tests.sh r04_final || exit 1
+# the chip ceilings the bench line quotes (built in the build container: hipcc -O3 tools/<x>.hip -o tools/<x>)
+timeout -k 10 60 ./tools/wrbench > $OUT/wrbench.txt 2>&1 || exit 6
+timeout -k 10 60 ./tools/aqbench > $OUT/aqbench.txt 2>&1 || exit 7
+timeout -k 10 60 ./tools/bqbench > $OUT/bqbench.txt 2>&1 || exit 8
 timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail $OUT/bench.err; exit 2; }
 for c in cfg2 cfg4 cfg5; do
   timeout -k 10 300 python bench.py --config $c --steps 200 --warmup 20 --no-cpu-baseline > $OUT/bench_$c.json 2> $OUT/bench_$c.err || { tail $OUT/bench_$c.err; exit 3; }
