@@ -158,7 +158,7 @@ struct OpSubTw {
 // z_b[n] and stores z_b at row b L + n of the scratch (sub-plane b); k_colsf runs L-point column tiles
 // over the scratch's sub-planes -- the N = 2048 column shape (8-column halves, XCD-paired: 64-byte
 // pieces of 128-byte lines) -- and writes row F m + b of the plane, permuted.  The 4-column tiles of a
-// whole 4096-point column (32-byte pieces, 0.57 of peak) are not needed.
+// whole 4096-point column (32-byte pieces, 0.57 of peak) are not needed (docs/MEASUREMENTS.md section 3).
 
 // k_rowsf: a one-row engine (N / 16 lanes); item n runs its rows n, n + L back to back with the next
 // row's loads in flight across each row's stages.  A lane's last-stage outputs sit at the same columns

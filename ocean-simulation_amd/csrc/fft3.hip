@@ -396,7 +396,7 @@ __global__ __launch_bounds__(2 * W * N / 8) void k_pass_b8(DevView v, int items)
     }
 }
 
-// Pass A over mirror pairs (N = 1024, P = 4; DESIGN.md "pass A4").  Item i of
+// Pass A over mirror pairs (N = 1024, P = 4; docs/MEASUREMENTS.md section 3, "pass A4").  Item i of
 // unit u covers rows y1 = i and y2 = N - i for 0 < i < N/2; item 0 covers rows
 // 0 and N/2, which are their own mirrors and are evolved texel by texel.  The
 // texel k = (x, y1) and its mirror -k = ((N - x) % N, y2) have the same |k|,
@@ -411,7 +411,7 @@ __global__ __launch_bounds__(2 * W * N / 8) void k_pass_b8(DevView v, int items)
 // PH = 2 planes per LDS pass: 4 of the 8 sequences in LDS (planes p0, p0 + 1 of both rows),
 // the stages run twice per item: 43.5 KiB of LDS instead of 78 KiB, so 3 workgroups share a
 // CU instead of 2 and the per-workgroup latency chain (evolve -> LDS stages -> stores)
-// overlaps better: 38.6 -> 33.0 us at cfg3.
+// overlaps better: 38.6 -> 33.0 us at cfg3 (docs/MEASUREMENTS.md).
 //
 // P = 2 (displacement-only frames, N = 256): both planes in one LDS pass.
 template <int N, bool BAND = false, int WT = 0, int P = 4>
@@ -549,7 +549,7 @@ __global__ __launch_bounds__(N / 4) void k_pass_a4(DevView v, float time, int it
     }
 }
 
-// Pass A8 (N = 512, two planes: small displacement-only jobs, cfg2): the
+// Pass A8 (N = 512, two planes: small displacement-only jobs, cfg2; docs/MEASUREMENTS.md section 6): the
 // mirror pairs of k_pass_a4 on N/2 lanes with 8 values each.  Lane j holds texels x = j, j + N/2
 // of row y1 and their mirrors in row y2 (butterfly jm = (N/2 - j) % (N/2)), so it evolves two
 // texel pairs instead of four; the row transform runs radix 2 in registers, then radix 8, 8
@@ -707,7 +707,7 @@ int grid3(K kernel, int threads, int items) {
     return items < g ? items : g;
 }
 
-// EPF at N = 4096: the next row's h0 in flight across the stages (641 against 658 us)
+// EPF at N = 4096: the next row's h0 in flight across the stages (641 against 658 us, docs/MEASUREMENTS.md)
 template <int N, int P, int RS, bool PF, bool BAND = false, int WT = 0>
 hipError_t go_a3k(const DevView& v, float t, hipStream_t s) {
     if constexpr (WT == 0 && N >= 128 && N <= 1024) {
@@ -818,7 +818,7 @@ bool pass_a4_supported(int n, int planes) {
 }
 
 // P = 2 at N = 512: pass A8 (256 lanes, 8 values each; 6.64 against 7.47 us for pass A4's two-plane
-// layout at cfg2)
+// layout at cfg2, docs/MEASUREMENTS.md section 6)
 hipError_t launch_pass_a_v4(const DevView& v, float t, hipStream_t s) {
     if (!pass_a4_supported(v.n, v.planes) || !v.h0k) return hipErrorInvalidValue;
     if (v.planes == 2) {

@@ -265,7 +265,7 @@ hipError_t go_c1(const DevView& v, hipStream_t s) {
     constexpr int T = kSeq * (N / kL1) / kElems;
     const int items = (Q ? 3 : v.planes) * v.units * (v.nx / kWT) * (kL1 / (kSeq / kWT));
     // two workgroups per CU, not the four that fit: cfg5 column passes 1.72 -> 1.67 ms
-    // (three per CU: 1.70 ms), DESIGN.md section 3
+    // (three per CU: 1.70 ms), docs/MEASUREMENTS.md section 3
     const int g = grid4(k_col4s1<N, Q>, T, items, 2);
     launch((k_col4s1<N, Q>), dim3(g), dim3(T), 0, s, v, items);
     return hipGetLastError();

@@ -1,5 +1,5 @@
 // The fused frame through a THREE-plane intermediate (N = 512 / 1024, full outputs):
-// pass AQ (mirror-pair rows) and pass BQ (column tiles).  DESIGN.md section 3, "Q schedule".
+// pass AQ (mirror-pair rows) and pass BQ (column tiles).  DESIGN.md section 3, "Three-plane frame".
 //
 // The reference transforms four packed planes (TimeDependentSpectrum.compute:42-45):
 //   P1 = Dx + i Dz,  P2 = Dy + i Dxz,  P3 = Dyx + i Dyz,  P4 = Dxx + i Dzz
@@ -50,7 +50,7 @@ __device__ __forceinline__ void q_planes(const Planes4& o, const Planes4& om, QT
 // (-kx, 1/|k|, -kz)): with P1..P4 of TimeDependentSpectrum.compute:29-45,
 //   Q1 = P1 = (i kx - kz) / |k| h,  Q2 = Y + i Dyx = (1 - kx) h,  Q3 = Dyz + i Dxx = i (kz - kx^2 / |k|) h,
 // and at -k the same with kx, kz negated and conj h: a complex scale of h each, 24 VALU for the pair
-// where planes_of twice + q_planes take ~80 (pass A is VALU-bound: SQ counters).  The
+// where planes_of twice + q_planes take ~80 (pass A is VALU-heavy: SQ counters, docs/MEASUREMENTS.md section 6).  The
 // same values in real arithmetic; in fp32 they round differently (parity tolerance, tests).
 __device__ __forceinline__ void q_fast(float2 h, float4 w, QTex& a, QTex& b) {
     const float c1x = -w.z * w.y, c1y = w.x * w.y;  // (i kx - kz) / |k|
@@ -741,7 +741,7 @@ hipError_t go_bq(const DevView& v, hipStream_t s) {
 }  // namespace
 
 // N = 2048 keeps the four-plane passes: pass A3Q's idle fourth sequence slot costs more there
-// than the column passes save (4 x 2048^2: 612 against 599 us per frame).
+// than the column passes save (4 x 2048^2: 612 against 599 us per frame; docs/MEASUREMENTS.md section 3).
 bool pass_q_supported(int n, int planes) { return planes == 4 && (n == 512 || n == 1024 || n == 4096); }
 
 hipError_t launch_pass_a_q(const DevView& v, float t, hipStream_t s) {

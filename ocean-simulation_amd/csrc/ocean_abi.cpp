@@ -426,7 +426,7 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
     c->opt = ocean_options::from_env();
     // Width of the fused path's column tiles.  With fewer tiles than CUs (one 512^2
     // cascade: 32 tiles of 16 columns) pass B ran on an eighth of the chip, so small
-    // jobs at N <= 512 take 4-column tiles (at N = 1024 pass A's
+    // jobs at N <= 512 take 4-column tiles (docs/MEASUREMENTS.md section 3; at N = 1024 pass A's
     // 32-byte tile rows cost what pass B gains).  OCEAN_TILE_W overrides (A/B).
     c->tile_w = ocean::fftcore::inter_w(n);
     {

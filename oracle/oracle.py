@@ -9,7 +9,7 @@ restatement whose 2D IFFT is numpy.fft (not the reference's butterfly
 schedule); it cross-checks the C oracle in tests/test_oracle.py.
 
 Parity status: "parity unpinned" by reference-produced vectors -- the reference
-(Unity/HLSL) ships none and cannot run here; see DESIGN.md section 3.
+(Unity/HLSL) ships none and cannot run here; see DESIGN.md section 2.
 """
 from __future__ import annotations
 
@@ -391,7 +391,7 @@ SCENE_CASCADES = [  # Waves.unity:1431-1435, 470-474, 1249-1253, 1572-1576
 
 
 def rel_err(a, b):
-    """Norm-relative error max|a-b| / max|b| (DESIGN.md section 3 tolerance definition)."""
+    """Norm-relative error max|a-b| / max|b| (DESIGN.md section 2 tolerance definition)."""
     a = np.asarray(a)
     b = np.asarray(b)
     den = np.abs(b).max()

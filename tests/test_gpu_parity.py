@@ -1,6 +1,6 @@
 """GPU parity tests: the HIP path (through the C ABI) against the CPU oracle.
 
-Tolerance (DESIGN.md section 3): every output channel of every cascade within
+Tolerance (DESIGN.md section 2): every output channel of every cascade within
 norm-relative error max|gpu - oracle| / max|oracle| <= 1e-5 (north_star: "fp32
 outputs within 1e-5 relative"); integer-exact quantities (noise, wave numbers,
 omega) bit-exact.  Run with `python -m pytest tests -m gpu` on an MI355X.

@@ -1,4 +1,4 @@
-// Pass BQ's memory shape without the FFT ("what holds pass BQ"): per item
+// Pass BQ's memory shape without the FFT ("What holds each hot kernel"; docs/MEASUREMENTS.md section 3): per item
 // (unit, 8-column tile) three 64 KiB tile-major plane blocks are read (24 B per texel), the foam
 // state read and written (4 + 4 B), and three float4 textures written (48 B), 4 x 1024^2 texels:
 // 335 MB per launch.  Variants of the texture stores only:

@@ -1,4 +1,4 @@
-// Launch-latency floor for small jobs (cfg2 analysis): the duration
+// Launch-latency floor for small jobs (cfg2 analysis, docs/MEASUREMENTS.md section 6): the duration
 // of back-to-back launches of (0) an empty kernel, (1) a kernel whose workgroups load one
 // 16 KiB block each and (2) load it, wait, and store it back elsewhere -- 256 workgroups of
 // 128 lanes, one item each, as pass A3 runs at cfg2.  Prints microseconds per launch.

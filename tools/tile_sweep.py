@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Wide vs narrow (4-column) tiles of the fused path on small jobs: pass A + pass B
 kernel time per frame for each (N, cascades, planes); OCEAN_TILE_W picks the width
-at ocean_create (narrow tiles)."""
+at ocean_create (docs/MEASUREMENTS.md section 3, narrow tiles)."""
 import os
 import sys
 

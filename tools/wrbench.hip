@@ -1,4 +1,4 @@
-// Write-side ceilings of pass B's traffic on MI355X ("where the frame's time
+// Write-side ceilings of pass B's traffic on MI355X (docs/MEASUREMENTS.md section 3, "where the frame's time
 // goes"): (1) streamed float4 stores alone, nontemporal and default policy, over pass B's 192 MiB
 // of textures; (2) a re-read of a 96 MiB buffer (the three-plane intermediate, Infinity-Cache
 // resident after its first pass) alone; (3) both at once in one kernel, the byte mix of pass BQ.
