@@ -327,8 +327,9 @@ def update_loop(steps=200, warmup=20):
     (WaterBody.Update, WaterBody.cs:284-297): CalculateWavesTexturesAtTime with the mip chains of DERIV
     and TURB regenerated every frame (GenerateMips, :191-192; OCEAN_F_MIPS), then one asynchronous
     readback of displacement slice 0 per frame (AsyncGPUReadback.Request, :288) into the facade's
-    pinned ring, polled, and copied out when it lands (request.GetData<Color>().ToArray(), :295) --
-    ocean_hip.WaterBody.Update.  Reported beside `value` (the device frame without mips):
+    pinned ring, polled, the landed slice kept in its pinned slot for GetWaterHeight (the reference
+    copies it out, request.GetData<Color>().ToArray(), :295; the facade's buoyancyData copies on
+    access) -- ocean_hip.WaterBody.Update.  Reported beside `value` (the device frame without mips):
     frames/s of that loop, its PCIe bytes per frame, the frame with mips alone, and the mip kernels' time
     per frame from HIP events."""
     wb = oh.scene_water_body(n=1024, n_cascades=4, seed=20251121).Awake()

@@ -49,10 +49,10 @@ public:
         ApplyParams();
         check(ocean_generate_noise(ctx_, seed), "ocean_generate_noise");
         check(ocean_init_spectrum(ctx_), "ocean_init_spectrum");
-        // the readback ring: maxReadbacksInFlight pinned slices allocated once and reused, freed only
-        // in OnDisable (hipHostFree synchronizes the device, so a free per request would make every
-        // Update wait for the frame it just queued)
-        for (size_t i = 0; i < std::max<size_t>(maxReadbacksInFlight, 1); ++i) {
+        // the readback ring: maxReadbacksInFlight pinned slices, plus the one the last landed slice stays
+        // in, allocated once and reused, freed only in OnDisable (hipHostFree synchronizes the device,
+        // so a free per request would make every Update wait for the frame it just queued)
+        for (size_t i = 0; i < std::max<size_t>(maxReadbacksInFlight, 1) + 1; ++i) {
             void* b = nullptr;
             check(ocean_host_alloc(SliceBytes(), &b), "ocean_host_alloc");
             free_.push_back(b);
@@ -103,7 +103,7 @@ public:
 
     // WaterBody.cs:195-209, with its mapping of world x, z over [-texturesSize/2, texturesSize/2].
     float GetWaterHeight(float worldX, float worldZ) const {
-        if (buoyancyData_.empty()) return 0.0f;
+        if (!held_) return 0.0f;
         auto inverse_lerp = [](float a, float b, float v) {
             return a == b ? 0.0f : std::min(std::max((v - a) / (b - a), 0.0f), 1.0f);
         };
@@ -112,7 +112,7 @@ public:
         const float v = inverse_lerp((float)(-n / 2), (float)(n / 2), worldZ);
         const int x = std::min(std::max((int)(u * n), 0), n - 1);
         const int y = std::min(std::max((int)(v * n), 0), n - 1);
-        return buoyancyData_[((size_t)y * n + x) * 4 + 1];  // .g = Dy
+        return held_[((size_t)y * n + x) * 4 + 1];  // .g = Dy
     }
 
     // What Water.shader reads at world positions (x, z, lod) -> 12 floats per point.
@@ -131,6 +131,11 @@ public:
     void OnDisable() {
         for (auto& p : readbacks_) ocean_readback_release(p.req);
         readbacks_.clear();
+        if (held_slot_) {  // the last landed slice outlives the pinned ring
+            last_.assign(held_, held_ + SliceBytes() / 4);
+            held_ = last_.data();
+            held_slot_ = nullptr;
+        }
         for (void* b : owned_) ocean_host_free(b);
         owned_.clear();
         free_.clear();
@@ -138,7 +143,11 @@ public:
         ctx_ = nullptr;
     }
 
-    const std::vector<float>& buoyancyData() const { return buoyancyData_; }
+    // The last landed displacement slice 0 (WaterBody.cs:295's array), a copy the caller owns as
+    // ToArray() gives; empty before the first readback lands.
+    std::vector<float> buoyancyData() const {
+        return held_ ? std::vector<float>(held_, held_ + SliceBytes() / 4) : std::vector<float>();
+    }
     long requested() const { return requested_; }
     long completed() const { return completed_; }
 
@@ -150,7 +159,9 @@ private:
     ocean_ctx* ctx_ = nullptr;
     std::deque<Pending> readbacks_;
     std::vector<void*> free_, owned_;  // pinned readback ring: idle slots, all slots
-    std::vector<float> buoyancyData_;
+    const float* held_ = nullptr;  // the last landed slice, in its pinned slot (out of the ring)
+    void* held_slot_ = nullptr;
+    std::vector<float> last_;  // the last slice after OnDisable
     long requested_ = 0, completed_ = 0;
 
     size_t SliceBytes() const { return (size_t)texturesSize * texturesSize * 16; }
@@ -166,13 +177,19 @@ private:
     void Complete(int st) {
         Pending p = readbacks_.front();
         readbacks_.pop_front();
-        if (st == 1) {
-            buoyancyData_.resize(SliceBytes() / 4);
-            std::memcpy(buoyancyData_.data(), p.buf, SliceBytes());
-            ++completed_;
-        }
         ocean_readback_release(p.req);
-        free_.push_back(p.buf);  // back to the ring
+        if (st == 1) {
+            // The reference copies every landed request out (request.GetData<Color>().ToArray(),
+            // :295): Unity's NativeArray lives only inside the callback.  The pinned slot outlives
+            // the request, so the slice stays in place and the slot leaves the ring until the next
+            // landed readback replaces it (no 16 MiB host copy per frame at 1024^2).
+            if (held_slot_) free_.push_back(held_slot_);
+            held_slot_ = p.buf;
+            held_ = static_cast<const float*>(p.buf);
+            ++completed_;
+        } else {
+            free_.push_back(p.buf);  // back to the ring
+        }
     }
 };
 

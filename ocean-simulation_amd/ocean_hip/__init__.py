@@ -373,9 +373,16 @@ class Readback:
     @property
     def data(self) -> np.ndarray:
         """A copy of the completed readback (waits if still pending)."""
+        return self.view().copy()
+
+    def view(self) -> np.ndarray:
+        """The completed readback in place, read-only, without a copy (waits if still pending).  Valid
+        while the pinned slot is neither released nor handed to another request."""
         self.wait()
         raw = (ctypes.c_float * (self.nbytes // 4)).from_address(self._buf.value)
-        return np.frombuffer(raw, np.float32).reshape(self.shape).copy()
+        v = np.frombuffer(raw, np.float32).reshape(self.shape)
+        v.flags.writeable = False
+        return v
 
     def release(self) -> None:
         if self._h:
@@ -439,10 +446,11 @@ class WaterBody:
 
     def __post_init__(self):
         self.ctx: Optional[OceanContext] = None
-        self.buoyancyData: Optional[np.ndarray] = None
+        self._buoy: Optional[np.ndarray] = None  # the last landed slice: a view of the held pinned slot
         self._readbacks: List[Readback] = []
         self._ring: List[PinnedBuffer] = []  # pinned readback slots, allocated in Awake
         self._idle: List[PinnedBuffer] = []
+        self._held: Optional[PinnedBuffer] = None  # the pinned slot the last landed slice stays in
 
     def params(self) -> dict:
         return dict(wind_speed=self.windSpeed, wind_dir_x=self.windDirection[0], wind_dir_y=self.windDirection[1],
@@ -462,8 +470,10 @@ class WaterBody:
             self.ctx.generate_noise(self.seed)
         self.ctx.init_spectrum()
         slice_bytes = self.texturesSize * self.texturesSize * 16
-        self._ring = [PinnedBuffer(slice_bytes) for _ in range(self.MAX_READBACKS_IN_FLIGHT)]
+        # one slot more than the requests in flight: the one the last landed slice stays in
+        self._ring = [PinnedBuffer(slice_bytes) for _ in range(self.MAX_READBACKS_IN_FLIGHT + 1)]
         self._idle = list(self._ring)
+        self._held = None
         return self
 
     def OnValidate(self) -> None:
@@ -475,7 +485,8 @@ class WaterBody:
     def CalculateWavesTexturesAtTime(self, time: float) -> None:
         self.ctx.step(time)
 
-    MAX_READBACKS_IN_FLIGHT = 8  # pinned ring slots = bound on queued requests (the reference's queue is engine-managed)
+    MAX_READBACKS_IN_FLIGHT = 8  # bound on queued requests (the reference's queue is engine-managed); the ring
+    # holds one pinned slot more, the one the last landed slice stays in
 
     def Update(self, time: float) -> None:
         """WaterBody.Update (WaterBody.cs:284-297): step, then issue a new AsyncGPUReadback
@@ -493,11 +504,25 @@ class WaterBody:
             raise
 
     def _complete(self, rb: "Readback") -> None:
-        self.buoyancyData = rb.data
+        # The reference copies every completed request out (request.GetData<Color>().ToArray(),
+        # WaterBody.cs:295): Unity's NativeArray lives only inside the callback.  A pinned ring slot
+        # outlives its request, so the landed slice stays in place instead: the slot leaves the
+        # ring until the next completed readback replaces it, GetWaterHeight reads it there, and
+        # buoyancyData copies it out only when a caller asks (16 MiB of host copy saved per frame
+        # at 1024^2).
+        view = rb.view()
         slot = rb.slot
         rb.release()
-        if slot is not None:
-            self._idle.append(slot)
+        if self._held is not None:
+            self._idle.append(self._held)
+        self._held = slot
+        self._buoy = view
+
+    @property
+    def buoyancyData(self) -> Optional[np.ndarray]:
+        """The last landed displacement slice 0, [y][x][rgba] (WaterBody.cs:295's array): a copy the
+        caller owns, as ToArray() gives."""
+        return None if self._buoy is None else np.array(self._buoy)
 
     def _poll_readbacks(self) -> None:
         while self._readbacks and self._readbacks[0].done():
@@ -511,7 +536,7 @@ class WaterBody:
     def GetWaterHeight(self, worldPosition) -> float:
         """WaterBody.cs:195-209, including its quirk of mapping world x,z over
         [-texturesSize/2, texturesSize/2] instead of the cascade length."""
-        if self.buoyancyData is None:
+        if self._buoy is None:
             return 0.0
         n = self.texturesSize
 
@@ -521,7 +546,7 @@ class WaterBody:
         v = inv_lerp(-(n // 2), n // 2, float(worldPosition[2]))
         x = min(max(int(u * n), 0), n - 1)
         y = min(max(int(v * n), 0), n - 1)
-        return float(self.buoyancyData[y, x, 1])
+        return float(self._buoy[y, x, 1])
 
     def SampleWorld(self, points, tile: int = 0) -> np.ndarray:
         """What Water.shader reads at world positions (x, z, lod): summed displacement,
@@ -542,9 +567,11 @@ class WaterBody:
         for rb in self._readbacks:
             rb.release()
         self._readbacks = []
+        if self._buoy is not None:  # the last landed slice outlives the pinned ring
+            self._buoy = np.array(self._buoy)
         for b in self._ring:
             b.release()
-        self._ring, self._idle = [], []
+        self._ring, self._idle, self._held = [], [], None
         if self.ctx is not None:
             self.ctx.close()
             self.ctx = None

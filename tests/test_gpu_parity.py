@@ -494,7 +494,21 @@ def test_water_body_facade_and_get_water_height():
     wb.Update(1.6)            # a later frame may still find the request in flight: never blocks
     wb.WaitForReadback()
     assert not np.array_equal(wb.DisplacementsTextures(), disp)
+    # the landed slice stays in its pinned slot (no copy per frame); buoyancyData is a copy the
+    # caller owns, as ToArray() gives: more frames than the ring holds leave a kept copy unchanged
+    kept = wb.buoyancyData
+    at_16 = wb.ctx.read(oh.TEX_DISP, 0, 0)
+    np.testing.assert_array_equal(kept, at_16)
+    for k in range(3 * wb.MAX_READBACKS_IN_FLIGHT):
+        wb.Update(2.0 + k / 60.0)
+    wb.WaitForReadback()
+    last = wb.ctx.read(oh.TEX_DISP, 0, 0)
+    np.testing.assert_array_equal(wb.buoyancyData, last)
+    assert wb.GetWaterHeight((3.0, 0.0, -7.0)) == last[121, 131, 1]  # world (3, -7) -> texel (131, 121)
+    assert not np.array_equal(kept, last)
+    np.testing.assert_array_equal(kept, at_16)
     wb.OnDisable()
+    assert wb.GetWaterHeight((3.0, 0.0, -7.0)) == last[121, 131, 1]  # the slice outlives the ring
 
 
 def test_state_errors():
