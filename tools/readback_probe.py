@@ -71,6 +71,33 @@ out["readback_ring_only_ms"] = timed(ring_only)
 for r in ring:
     r.wait()
     r.release()
+# the Update loop's shape at several ring depths (requests in flight), with and without the frames
+
+
+def ring_loop(depth, with_step, k=frames):
+    idle_slots, q = list(wb._ring[:depth]), []
+
+    def finish(r):
+        r.wait()
+        idle_slots.append(r.slot)
+        r.release()
+    t0 = time.perf_counter()
+    for f in range(k):
+        if with_step:
+            ctx.step(f / 60.0)
+        while q and q[0].done():
+            finish(q.pop(0))
+        if not idle_slots:
+            finish(q.pop(0))
+        q.append(ctx.read_async(oh.TEX_DISP, 0, 0, idle_slots.pop()))
+    while q:
+        finish(q.pop(0))
+    return (time.perf_counter() - t0) / k * 1e3
+
+
+for d in (1, 2, 4, 8):
+    out[f"ring{d}_readback_only_ms"] = ring_loop(d, False)
+    out[f"ring{d}_with_frames_ms"] = ring_loop(d, True)
 # frame + readback waited every frame (no overlap)
 out["step_then_readback_waited_ms"] = timed(lambda f: (ctx.step(f / 60.0), readback_only(f)))
 # host time of one Update call (the ring full: includes waiting for the oldest request)
