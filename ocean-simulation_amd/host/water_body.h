@@ -78,7 +78,9 @@ public:
             if (st == 0) break;
             Complete(st);
         }
-        if (free_.empty()) {  // every ring slot in flight: wait for the oldest request
+        // at most maxReadbacksInFlight requests queued (the ring's extra slot holds the landed slice):
+        // when full, wait for the oldest
+        while (!readbacks_.empty() && (readbacks_.size() >= std::max<size_t>(maxReadbacksInFlight, 1) || free_.empty())) {
             const int st = ocean_readback_wait(readbacks_.front().req) == OCEAN_OK ? 1 : -1;
             Complete(st);
         }

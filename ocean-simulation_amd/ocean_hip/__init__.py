@@ -494,7 +494,9 @@ class WaterBody:
         each completed one refreshes buoyancyData, as the reference's callback does (:292-295)."""
         self.CalculateWavesTexturesAtTime(time)
         self._poll_readbacks()
-        if not self._idle:  # every ring slot in flight: wait for the oldest request
+        # at most MAX_READBACKS_IN_FLIGHT requests queued (the ring's extra slot holds the landed slice):
+        # when full, wait for the oldest
+        while self._readbacks and (len(self._readbacks) >= self.MAX_READBACKS_IN_FLIGHT or not self._idle):
             self._complete(self._readbacks.pop(0))
         slot = self._idle.pop()
         try:

@@ -509,6 +509,13 @@ def test_water_body_facade_and_get_water_height():
     np.testing.assert_array_equal(kept, at_16)
     wb.OnDisable()
     assert wb.GetWaterHeight((3.0, 0.0, -7.0)) == last[121, 131, 1]  # the slice outlives the ring
+    # 16 MiB slices queue faster than they land: the ring fills before the first request completes
+    big = oh.scene_water_body(n=1024, n_cascades=1, seed=7).Awake()
+    for k in range(3 * big.MAX_READBACKS_IN_FLIGHT):
+        big.Update(k / 60.0)
+    big.WaitForReadback()
+    np.testing.assert_array_equal(big.buoyancyData, big.ctx.read(oh.TEX_DISP, 0, 0))
+    big.OnDisable()
 
 
 def test_state_errors():
