@@ -77,7 +77,9 @@ namespace OceanHip
         // displacement slice 0 EVERY frame (AsyncGPUReadback.Request, :288); requests
         // complete in order and each completed one refreshes buoyancyData, as the
         // reference's callback does (:292-295).  Requests land in slots of a pinned ring.
-        const int MaxReadbacksInFlight = 8;  // ring slots; the reference's request queue is engine-managed
+        const int MaxReadbacksInFlight = 4;  // ring slots; the reference's request queue is engine-managed.
+                                             // 2-4 in flight keep the 16 MiB copies back to back beside the
+                                             // frames; 8 stretch each copy 2.5x (DESIGN.md section 1)
         readonly System.Collections.Generic.Queue<(IntPtr req, IntPtr buf)> readbacks =
             new System.Collections.Generic.Queue<(IntPtr req, IntPtr buf)>();
         readonly System.Collections.Generic.List<IntPtr> ring = new System.Collections.Generic.List<IntPtr>();

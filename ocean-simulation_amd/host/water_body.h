@@ -37,7 +37,8 @@ public:
     std::vector<WaterCascade> cascades{WaterCascade{}};
     uint64_t seed = 20251121;  // the reference's UnityEngine.Random is unseeded; this library's generator is
     int device = 0;
-    size_t maxReadbacksInFlight = 8;  // pinned ring slots = bound on queued requests (set before Awake)
+    size_t maxReadbacksInFlight = 4;  // bound on queued requests (set before Awake): 2-4 keep the copies back to
+                                      // back beside the frames; 8 stretch each
 
     WaterBody() = default;
     WaterBody(const WaterBody&) = delete;

@@ -485,8 +485,11 @@ class WaterBody:
     def CalculateWavesTexturesAtTime(self, time: float) -> None:
         self.ctx.step(time)
 
-    MAX_READBACKS_IN_FLIGHT = 8  # bound on queued requests (the reference's queue is engine-managed); the ring
-    # holds one pinned slot more, the one the last landed slice stays in
+    # Bound on queued requests (the reference's queue is engine-managed); the ring holds one pinned slot
+    # more, the one the last landed slice stays in.  Measured at cfg3 (tools/readback_probe.py): 2-4 in
+    # flight keep the 16 MiB copies back to back beside the frames, 0.33 ms per frame; 8 in flight run
+    # 0.82 ms per frame, each copy stretched to 2.5x its time alone.
+    MAX_READBACKS_IN_FLIGHT = 4
 
     def Update(self, time: float) -> None:
         """WaterBody.Update (WaterBody.cs:284-297): step, then issue a new AsyncGPUReadback
