@@ -141,6 +141,25 @@ def find_record(config, symbol, profiles_dir=PROFILES):
     return best
 
 
+def entry_record(config, symbol, profiles_dir=PROFILES):
+    """The record of one timed entry of a kernel kind (find_record per kernel, summed): one kernel, except
+    the N >= 2048 column passes, where each (unit, band) entry launches C1 (k_col4s1) then C2 (k_col4s2,
+    the symbol the library reports as the kind's last kernel).  None unless every kernel of the entry
+    has a record, all in one directory."""
+    syms = [symbol] if symbol else []
+    if symbol and "k_col4s2<" in symbol:
+        syms = [re.sub(r"k_col4s2<(\d+), \d+, ", r"k_col4s1<\1, ", symbol), symbol]
+    recs = [find_record(config, sym, profiles_dir) for sym in syms]
+    if not recs or not all(recs) or len({r["dir"] for r in recs}) != 1:
+        return None
+    record = dict(recs[-1])
+    record["avg_us"] = sum(r["avg_us"] for r in recs)
+    tb = [r["traffic_bytes_per_launch"] for r in recs]
+    record["traffic_bytes_per_launch"] = sum(tb) if all(t is not None for t in tb) else None
+    record["kernels"] = syms
+    return record
+
+
 def _round_dirs(profiles_dir):
     """This round's profile directories (profiles/<ROUND>*), oldest first by their stamp: micro-benchmark
     ceilings are quoted only when they were measured beside this round's kernels."""
@@ -589,20 +608,7 @@ def main():
         if rank == 0 and world == 1 and args.config == "cfg3" and not args.no_beyond_cache:
             ifft_stage["beyond_cache"] = ifft_beyond_cache()
 
-    # the kernels of one timed entry of the dominant kind: one kernel, except the N >= 2048 column passes,
-    # where each (unit, band) entry launches C1 (k_col4s1) then C2 (k_col4s2, the symbol the library
-    # reports as the kind's last kernel); the record's figures are summed over the entry's kernels
-    entry_syms = [dom_sym] if dom_sym else []
-    if dom_sym and "k_col4s2<" in dom_sym:
-        entry_syms = [re.sub(r"k_col4s2<(\d+), \d+, ", r"k_col4s1<\1, ", dom_sym), dom_sym]
-    recs = [find_record(args.config, sym) for sym in entry_syms] if not args.unfused else []
-    record = None
-    if recs and all(recs) and len({r["dir"] for r in recs}) == 1:
-        record = dict(recs[-1])
-        record["avg_us"] = sum(r["avg_us"] for r in recs)
-        tb = [r["traffic_bytes_per_launch"] for r in recs]
-        record["traffic_bytes_per_launch"] = sum(tb) if all(t is not None for t in tb) else None
-        record["kernels"] = entry_syms
+    record = entry_record(args.config, dom_sym) if not args.unfused else None
     traffic = record["traffic_bytes_per_launch"] if record else None
     # the dominant kernel's store stream against the chip's measured store ceiling: pass B writes the
     # textures (16 B DISP [+ 32 B DERIV, TURB] [+ 16 B NORMAL]) and the 4-B foam state per texel

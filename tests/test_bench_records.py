@@ -100,3 +100,21 @@ def test_mip_record_per_frame(bench, tmp_path, monkeypatch):
     assert r["us_per_frame"] == 36.0 and r["match"] == "lib" and set(r["kernels"]) == {"k_mips_block", "k_mips_tail"}
     _rec(tmp_path / "r04c", "cfg3", {blk: (1.0, 1), tail: (1.0, 1)}, lib="LIB", utc="2027-01-01T00:00:00Z")
     assert bench.mip_record(str(tmp_path))["dir"] == "profiles/r04u"  # another config's record never stands in
+
+
+def test_entry_record_sums_the_four_step_pair(bench, tmp_path, monkeypatch):
+    """At N >= 2048 one timed column entry launches C1 then C2; the library names C2.  The entry's
+    rocprofv3 time and PMC traffic are the two records summed (round 3 compared C2 alone with the
+    entry's bytes, a 1.16 'fraction')."""
+    monkeypatch.setattr(bench, "_IDENT", {"lib": "LIB", "src": "SRC"})
+    c1 = "void ocean::(anonymous namespace)::k_col4s1<4096, true>(ocean::DevView, int)"
+    c2 = "void ocean::(anonymous namespace)::k_col4s2<4096, 4, true>(ocean::DevView, int)"
+    _rec(tmp_path / "r04c5", "cfg5", {c1: (84000.0, 470), c2: (130000.0, 739)}, lib="LIB")
+    r = bench.entry_record("cfg5", c2, str(tmp_path))
+    assert r["avg_us"] == 214.0 and r["traffic_bytes_per_launch"] == 1209 and r["kernels"] == [c1, c2]
+    assert bench.entry_record("cfg5", SYM_BQ, str(tmp_path)) is None
+    _rec(tmp_path / "r04c3", "cfg3", {SYM_BQ: (55000.0, 336)}, lib="LIB")
+    r = bench.entry_record("cfg3", SYM_BQ, str(tmp_path))
+    assert r["avg_us"] == 55.0 and r["kernels"] == [SYM_BQ]
+    _rec(tmp_path / "r04c5b", "cfg5", {c2: (1.0, 1)}, lib="LIB", utc="2027-01-01T00:00:00Z")  # C2 alone, newer
+    assert bench.entry_record("cfg5", c2, str(tmp_path)) is None  # the pair's records sit in two directories
