@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """Benchmark of the per-frame ocean path on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg3|cfg2|cfg4|cfg5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg3|cfg1|cfg2|cfg4|cfg5]
+
+cfg1 (BASELINE.json configs[0], 256^2 x 1 on the scalar CPU path, no GPU) prints its own line with
+n_gpus 0: the C port timed as the labelled stand-in for the C# path (run_cfg1).
 
 A "step" is one ocean frame: ocean_step(t) = evolve -> 2D IFFT of every plane
 -> fill/foam for every (tile, cascade) unit the rank owns (WaterBody.cs:180-193
@@ -46,6 +49,8 @@ SCENE_CASCADES = [  # Assets/Scenes/Waves.unity (+ unreferenced 4th cascade :157
 
 # BASELINE.json configs (tiles are per job; sharded over ranks)
 CONFIGS = {
+    "cfg1": dict(n=256, cascades=1, tiles=1, disp_only=False, per_rank=True, cpu_only=True,
+                 desc="1 x 256^2 cascade, JONSWAP/TMA spectrum + 2D IFFT on the scalar CPU path (no GPU)"),
     "cfg2": dict(n=512, cascades=1, tiles=1, disp_only=True, per_rank=True,
                  desc="1 x 512^2 cascade, displacement only"),
     "cfg3": dict(n=1024, cascades=4, tiles=1, disp_only=False, per_rank=True,
@@ -70,15 +75,6 @@ def algorithmic_bytes(ctx):
     return {"pass_a": a, "pass_b": b, "frame": a + b, "cache_resident": resident}
 
 
-def _current_round(root=ROOT):
-    """This round's tag: one past the newest BENCH_rNN.json the driver has recorded (r04 while
-    BENCH_r03.json is the newest), so profiles/<ROUND>* never needs editing between rounds."""
-    import re
-    done = [int(m.group(1)) for f in os.listdir(root) for m in [re.match(r"BENCH_r(\d+)\.json$", f)] if m]
-    return f"r{(max(done) + 1 if done else 1):02d}"
-
-
-ROUND = _current_round()  # profiles/<ROUND>*/ hold this round's micro-benchmark records
 PROFILES = os.path.join(ROOT, "profiles")
 
 
@@ -160,58 +156,58 @@ def entry_record(config, symbol, profiles_dir=PROFILES):
     return record
 
 
-def _round_dirs(profiles_dir):
-    """This round's profile directories (profiles/<ROUND>*), oldest first by their stamp: micro-benchmark
-    ceilings are quoted only when they were measured beside this round's kernels."""
+def _ceiling_dirs(fname, profiles_dir):
+    """Directories holding the micro-benchmark record `fname` (wrbench.txt, aqbench.txt, bqbench.txt)
+    with a ceilings.json stamp (tools/stamp.py --ceilings), best first: records made by the current
+    code of the tool before others, then the newest stamp (UTC).  Directory names play no part, so the
+    quoted ceilings do not depend on the round."""
     if not os.path.isdir(profiles_dir):
         return []
-
-    def utc(d):  # stamped directories in stamp order (tools/stamp.py), unstamped ones first
-        f = os.path.join(profiles_dir, d, "stamp.json")
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import stamp as st
+    tool = st.CEILING_TOOLS[fname]
+    tool_path = os.path.join(ROOT, "tools", tool)
+    cur = st.code_sha(tool_path) if os.path.exists(tool_path) else None
+    found = []
+    for d in os.listdir(profiles_dir):
+        sp = os.path.join(profiles_dir, d, "ceilings.json")
+        if not (os.path.exists(os.path.join(profiles_dir, d, fname)) and os.path.exists(sp)):
+            continue
         try:
-            return json.load(open(f)).get("utc", "") if os.path.exists(f) else ""
+            s = json.load(open(sp))
         except Exception:
-            return ""
-    return sorted((d for d in os.listdir(profiles_dir) if d.startswith(ROUND)), key=lambda d: (utc(d), d))
+            continue
+        match = cur is not None and s.get("tool_code_sha256", {}).get(tool) == cur
+        found.append(((match, s.get("utc", "")), d))
+    return [d for _, d in sorted(found, reverse=True)]
 
 
 def write_ceilings(profiles_dir=os.path.join(ROOT, "profiles")):
-    """Measured store-bandwidth ceilings of this chip from this round's newest tools/wrbench.hip run
-    (profiles/<ROUND>*/wrbench.txt): GB/s of nontemporal float4 stores over 192 MiB (pass B's texture
-    bytes) and beyond the Infinity Cache (1 GiB).  None if this round has none."""
-    import re
-    best = None
-    for d in _round_dirs(profiles_dir):
-        f = os.path.join(profiles_dir, d, "wrbench.txt")
-        if not os.path.exists(f):
-            continue
+    """Measured store-bandwidth ceilings of this chip from the best stamped tools/wrbench.hip record
+    (_ceiling_dirs): GB/s of nontemporal float4 stores over 192 MiB (pass B's texture bytes) and
+    beyond the Infinity Cache (1 GiB).  None if no stamped record exists."""
+    for d in _ceiling_dirs("wrbench.txt", profiles_dir):
         got = {}
-        for line in open(f):
+        for line in open(os.path.join(profiles_dir, d, "wrbench.txt")):
             m = re.match(r"(write \w+ (?:192 MiB|1 GiB))\s+grid\s+\d+\s+[\d.]+ us\s+([\d.]+) GB/s", line)
             if m:
                 got[m.group(1)] = float(m.group(2))
         if "write nt 192 MiB" in got:
-            best = {"nt_192MiB_GBs": got["write nt 192 MiB"], "nt_beyond_cache_GBs": got.get("write nt 1 GiB"),
+            return {"nt_192MiB_GBs": got["write nt 192 MiB"], "nt_beyond_cache_GBs": got.get("write nt 1 GiB"),
                     "source": f"profiles/{d}/wrbench.txt"}
-    return best
+    return None
 
 
 def shape_us(fname, label, profiles_dir=os.path.join(ROOT, "profiles")):
-    """Microsecond time of the line starting with `label` in this round's newest
-    profiles/<ROUND>*/<fname> (tools/aqbench.hip, tools/bqbench.hip: a pass's memory shape run
-    without its evolve / FFT work, 4 x 1024^2).  (us, source) or None."""
-    import re
-    best = None
-    for d in _round_dirs(profiles_dir):
-        f = os.path.join(profiles_dir, d, fname)
-        if not os.path.exists(f):
-            continue
-        for line in open(f):
+    """Microsecond time of the line starting with `label` in the best stamped <fname> record
+    (_ceiling_dirs; tools/aqbench.hip, tools/bqbench.hip: a pass's memory shape run without its
+    evolve / FFT work, 4 x 1024^2).  (us, source) or None."""
+    for d in _ceiling_dirs(fname, profiles_dir):
+        for line in open(os.path.join(profiles_dir, d, fname)):
             m = re.match(re.escape(label) + r"\s+([\d.]+) us", line)
             if m:
-                best = (float(m.group(1)), f"profiles/{d}/{fname}")
-                break
-    return best
+                return float(m.group(1)), f"profiles/{d}/{fname}"
+    return None
 
 
 def beyond_cache(steps=20):
@@ -341,6 +337,41 @@ def mip_record(profiles_dir=PROFILES):
                         for nm, r in recs.items()}}
 
 
+UPDATE_WARM_S = 0.5  # Update-loop warm-up, wall seconds (update_loop)
+
+
+def numa_placement(device, host_ptrs):
+    """NUMA nodes that set the readback link rate: the GPU's (sysfs, from its PCI address), the calling
+    CPU's, and the node of the first page of each pinned host buffer (get_mempolicy(MPOL_F_NODE |
+    MPOL_F_ADDR)).  A pinned ring on the far socket crosses the inter-socket link (tools/d2hbench.hip
+    measures both placements); None where the system does not say."""
+    import ctypes
+    out = {"gpu_node": None, "cpu": None, "cpu_node": None, "pinned_page_nodes": []}
+    try:
+        pr = torch.cuda.get_device_properties(device)
+        bus = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+        out["gpu_pci"] = bus
+        out["gpu_node"] = int(open(f"/sys/bus/pci/devices/{bus}/numa_node").read())
+    except Exception:
+        pass
+    try:
+        libc = ctypes.CDLL(None, use_errno=True)
+        cpu = libc.sched_getcpu()
+        out["cpu"] = cpu
+        for node in range(64):
+            if os.path.exists(f"/sys/devices/system/node/node{node}/cpu{cpu}"):
+                out["cpu_node"] = node
+                break
+        for p in host_ptrs:
+            node = ctypes.c_int(-1)
+            r = libc.syscall(ctypes.c_long(239), ctypes.byref(node), None, ctypes.c_ulong(0), ctypes.c_void_p(p),
+                             ctypes.c_ulong(3))  # SYS_get_mempolicy (x86_64), MPOL_F_NODE | MPOL_F_ADDR
+            out["pinned_page_nodes"].append(node.value if r == 0 else None)
+    except Exception:
+        pass
+    return out
+
+
 def update_loop(steps=200, warmup=20):
     """The reference's per-frame loop at cfg3, as a Unity host over this library runs it
     (WaterBody.Update, WaterBody.cs:284-297): CalculateWavesTexturesAtTime with the mip chains of DERIV
@@ -350,42 +381,84 @@ def update_loop(steps=200, warmup=20):
     copies it out, request.GetData<Color>().ToArray(), :295; the facade's buoyancyData copies on
     access) -- ocean_hip.WaterBody.Update.  Reported beside `value` (the device frame without mips):
     frames/s of that loop, its PCIe bytes per frame, the frame with mips alone, and the mip kernels' time
-    per frame from HIP events."""
+    per frame from HIP events.
+    Warm-up is by time, not by count: the loop's first frames in a process run 3-13x slower
+    (tools/update_ramp.py, docs/MEASUREMENTS.md section 8), so a count sized for --steps 500 left the
+    driver's --steps 20 --warmup 5 timing the ramp (1.09 k against 3.02 k frames/s).  Both the frame
+    and the loop run for >= UPDATE_WARM_S (and >= `warmup` frames) before their timed regions.
+    Attribution: `d2h` = the device-to-host copies' own duration (ocean_readback_copy_ms: events on the
+    copy stream around each copy) -> the link's GB/s; `kernel_us_in_loop` = the frame's kernels timed
+    inside the loop (HIP events), against `step_with_mips.kernel_us`; `numa` = where the GPU, the
+    calling CPU and the pinned ring sit."""
     wb = oh.scene_water_body(n=1024, n_cascades=4, seed=20251121).Awake()
     ctx = wb.ctx
     try:
-        for f in range(warmup):
+        f = 0
+        w0 = time.perf_counter()
+        while f < warmup or time.perf_counter() - w0 < UPDATE_WARM_S:
             ctx.step(f / 60.0)
+            f += 1
+            if f % 16 == 0:
+                ctx.synchronize()
         ctx.synchronize()
         t0 = time.perf_counter()
-        for f in range(steps):
-            ctx.step((warmup + f) / 60.0)
+        for k in range(steps):
+            ctx.step((f + k) / 60.0)
         ctx.synchronize()
         step_s = (time.perf_counter() - t0) / steps
         ctx.set_kernel_timing(True)
         ctx.kernel_stats(0), ctx.kernel_stats(1), ctx.kernel_stats(2)
-        for f in range(steps):
-            ctx.step((warmup + f) / 60.0)
+        for k in range(steps):
+            ctx.step((f + k) / 60.0)
         ka, _ = ctx.kernel_stats(0)
         kb, _ = ctx.kernel_stats(1)
         km, nm = ctx.kernel_stats(2)
         ctx.set_kernel_timing(False)
         mips_sym = ctx.kernel_name(2)
-        for f in range(warmup):
+        # the loop: warm-up by time, then `steps` timed Update frames
+        f = 0
+        w0 = time.perf_counter()
+        while f < max(warmup, 2 * len(wb._ring)) or time.perf_counter() - w0 < UPDATE_WARM_S:
             wb.Update(f / 60.0)
+            f += 1
         wb.WaitForReadback()
+        warm_frames, warm_s = f, time.perf_counter() - w0
+        wb.readback_copy_ms = []
         t0 = time.perf_counter()
-        for f in range(steps):
-            wb.Update((warmup + f) / 60.0)
+        for k in range(steps):
+            wb.Update((f + k) / 60.0)
         wb.WaitForReadback()  # every requested readback has landed inside the timed region
         loop_s = (time.perf_counter() - t0) / steps
+        copies = list(wb.readback_copy_ms)
+        wb.readback_copy_ms = None
+        # the same loop again with the frame's kernels timed (HIP events): are the frames stretched by
+        # the copies beside them?
+        ctx.set_kernel_timing(True)
+        ctx.kernel_stats(0), ctx.kernel_stats(1), ctx.kernel_stats(2)
+        for k in range(steps):
+            wb.Update((f + steps + k) / 60.0)
+        wb.WaitForReadback()
+        la, _ = ctx.kernel_stats(0)
+        lb, _ = ctx.kernel_stats(1)
+        lm, _ = ctx.kernel_stats(2)
+        ctx.set_kernel_timing(False)
         slice_bytes = 1024 * 1024 * 16
         mips_rec = mip_record()
+        copy_ms = float(np.median(copies)) if copies else None
+        numa = numa_placement(wb.device, [b.ptr.value for b in wb._ring])
         return {"workload": "cfg3 (4 x 1024^2) frame + GenerateMips of DERIV and TURB + AsyncGPUReadback of "
                             "DISP slice 0 every frame, ocean_hip.WaterBody.Update (WaterBody.cs:284-297)",
                 "frames_per_s": round(1.0 / loop_s, 2), "ms_per_frame": round(1e3 * loop_s, 4),
+                "timed_frames": steps, "warmup": {"frames": warm_frames, "seconds": round(warm_s, 3)},
                 "pcie_bytes_per_frame": slice_bytes, "pcie_GBs": round(slice_bytes / loop_s / 1e9, 2),
-                "readback_ring_slots": wb.MAX_READBACKS_IN_FLIGHT,
+                "readback_ring_slots": wb._in_flight(),
+                "d2h": {"copies": len(copies), "median_ms": round(copy_ms, 4) if copy_ms else None,
+                        "max_ms": round(max(copies), 4) if copies else None,
+                        "GBs": round(slice_bytes / (copy_ms * 1e-3) / 1e9, 2) if copy_ms else None,
+                        "how": "ocean_readback_copy_ms: HIP events on the copy stream around each device-to-host copy"},
+                "kernel_us_in_loop": {"pass_a": round(1e3 * la / steps, 2), "pass_b": round(1e3 * lb / steps, 2),
+                                      "mips": round(1e3 * lm / steps, 2)},
+                "numa": numa,
                 "step_with_mips": {"frames_per_s": round(1.0 / step_s, 2), "ms_per_frame": round(1e3 * step_s, 4),
                                    "kernel_us": {"pass_a": round(1e3 * ka / steps, 2), "pass_b": round(1e3 * kb / steps, 2),
                                                  "mips": round(1e3 * km / steps, 2)},
@@ -443,6 +516,55 @@ def cpu_baseline(cfg, frames=3):
             "multicore": multi}
 
 
+def run_cfg1(args):
+    """BASELINE.json configs[0]: one 256^2 cascade through the reference path on the scalar CPU, no GPU
+    (WaterBody.cs:171-193 on one core).  The path timed is the C port (oracle/ocean_oracle.c, the
+    reference's four kernels in their op order, radix-2 schedule included), standing in, labelled, for
+    the C# scalar re-implementation ocean-simulation_amd/csharp/CpuOcean.cs, which cannot run here: no
+    dotnet on this image.  `value` = frames/s of CalculateWavesTexturesAtTime (evolve, 4 x 2D IFFT, fill
+    and foam) over K timed frames after W warm-up frames; the initial spectrum (JONSWAP / TMA / spread,
+    CalculateInitialSpectrumTextures) is timed once beside it.  n_gpus is 0."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    cfg = CONFIGS["cfg1"]
+    n, C = cfg["n"], cfg["cascades"]
+    O.set_threads(1)
+    noise = O.generate_noise(n, 20251121)
+    t0 = time.perf_counter()
+    oc = O.OracleOcean(n, SCENE_PARAMS, SCENE_CASCADES[:C], noise)
+    init_s = time.perf_counter() - t0
+    for f in range(args.warmup):
+        oc.step(f / 60.0)
+    t0 = time.perf_counter()
+    for f in range(args.steps):
+        oc.step((args.warmup + f) / 60.0)
+    elapsed = time.perf_counter() - t0
+    return {
+        "metric": f"ocean-surface frames/sec ({cfg['desc']})",
+        "value": round(args.steps / elapsed, 2),
+        "unit": "frames/s",
+        "n_gpus": 0,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": None,
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (scene parameters of Waves.unity, seeded noise 20251121)",
+        "config": {"workload": f"cfg1: {cfg['desc']}", "n": n, "cascades": C, "tiles_per_gpu": None,
+                   "parallelism": "one host core, no GPU"},
+        "path": {"kind": "port", "cores": 1,
+                 "what": "C port of the reference path (oracle/ocean_oracle.c, -O2 -ffp-contract=off), standing in "
+                         "for the C# scalar path ocean-simulation_amd/csharp/CpuOcean.cs (same op order), which "
+                         "cannot run here: no dotnet on this image",
+                 "reference": "WaterBody.cs:171-193 (Awake's CalculateInitialSpectrumTextures, then "
+                              "CalculateWavesTexturesAtTime per frame)"},
+        "init_spectrum_ms": round(1e3 * init_s, 3),
+        "roofline": None,  # no GPU kernel runs in this config
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -459,6 +581,9 @@ def main():
     ap.add_argument("--only-update-loop", action="store_true",
                     help="run update_loop alone and print its JSON (the rocprofv3 record of the mip kernels)")
     args = ap.parse_args()
+    if CONFIGS[args.config].get("cpu_only"):
+        print(json.dumps(run_cfg1(args)), flush=True)
+        return
     if args.only_update_loop:
         print(json.dumps(update_loop(max(50, args.steps // 2), args.warmup)))
         return

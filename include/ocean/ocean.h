@@ -22,6 +22,11 @@
  *     ocean_generate_noise block the calling thread.
  *   - A context is not thread-safe: drive it from one thread (like Unity's
  *     main thread).  Multi-GPU = one context per device.
+ *   - The calling thread's current HIP device is never changed: a call makes
+ *     its context's device current for the span of the call and restores the
+ *     caller's device before it returns (ocean_create / ocean_destroy /
+ *     ocean_readback_release included).  One thread may drive contexts on
+ *     several devices, beside torch or any other HIP user, in any order.
  *
  * Memory layout in HBM (all fp32, texture index = [unit][y][x], unit = tile*C + cascade,
  * matching Unity's Tex2DArray [slice][y][x] with id.x = x):
@@ -48,8 +53,10 @@ extern "C" {
  *      return E_STATE before ocean_init_spectrum and the device entry checks alignment.
  *      New: ocean_reset_foam, ocean_set_column_band, ocean_sample_world(_device),
  *      ocean_read_async family, ocean_host_alloc/free, ocean_generate_noise_device,
- *      ocean_kernel_name, ocean_set_column_parity. */
-#define OCEAN_ABI_VERSION 2
+ *      ocean_kernel_name, ocean_set_column_parity.
+ *   3  semantics changed: no call moves the calling thread's current HIP device any more
+ *      (Conventions).  New: ocean_readback_copy_ms. */
+#define OCEAN_ABI_VERSION 3
 
 /* status codes */
 #define OCEAN_OK 0
@@ -293,6 +300,11 @@ int ocean_read_async(ocean_ctx *ctx, int texture, int tile, int cascade, void *d
 int ocean_readback_status(ocean_readback *rb);
 int ocean_readback_wait(ocean_readback *rb);
 void ocean_readback_release(ocean_readback *rb);
+/* Duration of a completed request's device-to-host copy in ms (HIP events on the copy stream around
+ * the copy itself: the link's share of the request, without the wait for the queued frames or the
+ * on-device snapshot).  OCEAN_E_STATE while the request is pending.  No reference counterpart:
+ * AsyncGPUReadback exposes no timing; hosts use it to attribute a readback-bound loop. */
+int ocean_readback_copy_ms(ocean_readback *rb, float *ms);
 
 /* Pinned host memory for ocean_read_async destinations (hipHostMalloc). */
 int ocean_host_alloc(size_t bytes, void **out);

@@ -115,6 +115,8 @@ namespace OceanHip
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
         public static extern void ocean_readback_release(IntPtr request);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
+        public static extern OceanStatus ocean_readback_copy_ms(IntPtr request, out float ms);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
         public static extern OceanStatus ocean_host_alloc(UIntPtr bytes, out IntPtr ptr);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
         public static extern void ocean_host_free(IntPtr ptr);

@@ -262,13 +262,45 @@ struct ocean_ctx {
 
 namespace {
 
-// Set the device for the calling thread and check the context.
-int enter(ocean_ctx* ctx) {
-    if (!ctx) return fail(OCEAN_E_INVALID_ARG, "null context");
-    hipError_t e = hipSetDevice(ctx->device);
-    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
-    return OCEAN_OK;
-}
+// Makes a device current for the span of one entry point and gives the calling thread its own
+// current device back on return (ocean.h, "Conventions"): a host that drives several contexts from
+// one thread, or runs torch in the same process, never sees its current device move.  hipSetDevice
+// is called only when the device differs.
+class DeviceScope {
+  public:
+    explicit DeviceScope(int device) {
+        if (hipGetDevice(&prev_) != hipSuccess) prev_ = -1;
+        if (prev_ == device) return;
+        const hipError_t e = hipSetDevice(device);
+        if (e != hipSuccess) {
+            status_ = hip_fail(e, "hipSetDevice");
+            return;
+        }
+        restore_ = prev_ >= 0;
+    }
+    ~DeviceScope() {
+        if (restore_) (void)hipSetDevice(prev_);
+    }
+    DeviceScope(const DeviceScope&) = delete;
+    DeviceScope& operator=(const DeviceScope&) = delete;
+    int status() const { return status_; }
+
+  private:
+    int prev_ = -1;
+    bool restore_ = false;
+    int status_ = OCEAN_OK;
+};
+
+}  // namespace
+
+// Entry of every call that touches the device: check the context, make its device current until the
+// call returns (DeviceScope), or return the failure.
+#define OCEAN_ENTER(ctx)                                                        \
+    if (!(ctx)) return fail(OCEAN_E_INVALID_ARG, "null context");              \
+    DeviceScope device_scope_((ctx)->device);                                   \
+    if (const int device_scope_status_ = device_scope_.status()) return device_scope_status_
+
+namespace {
 
 // Folds timed launches into kind_ms / kind_count and returns their events to the pool.
 // wait: synchronize the stream first (every pending launch is then finished); else fold
@@ -408,8 +440,8 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
     hipError_t e = hipGetDeviceCount(&ndev);
     if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
     if (device < 0 || device >= ndev) return fail(OCEAN_E_INVALID_ARG, "device index out of range");
-    e = hipSetDevice(device);
-    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    DeviceScope device_scope(device);  // the caller's current device is restored on return
+    if (const int r = device_scope.status()) return r;
 
     ocean_ctx* c = new (std::nothrow) ocean_ctx();
     if (!c) return fail(OCEAN_E_OUT_OF_MEMORY, "host allocation failed");
@@ -519,14 +551,14 @@ int ocean_create(int device, int n, int n_cascades, int n_tiles, uint32_t flags,
 
 void ocean_destroy(ocean_ctx* ctx) {
     if (!ctx) return;
-    (void)hipSetDevice(ctx->device);
+    DeviceScope device_scope(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     free_all(ctx);
     delete ctx;
 }
 
 int ocean_set_params(ocean_ctx* ctx, const ocean_params* params, const ocean_cascade* cascades) {
-    if (int r = enter(ctx)) return r;
+    OCEAN_ENTER(ctx);
     if (!params || !cascades) return fail(OCEAN_E_INVALID_ARG, "null params/cascades");
     const ocean_params& p = *params;
     if (!(p.gravity > 0) || !(p.fetch > 0) || !(p.wind_speed > 0) || !std::isfinite(p.depth))
@@ -551,7 +583,7 @@ int ocean_set_params(ocean_ctx* ctx, const ocean_params* params, const ocean_cas
 }
 
 int ocean_set_noise(ocean_ctx* ctx, int tile, const float* rg) {
-    if (int r = enter(ctx)) return r;
+    OCEAN_ENTER(ctx);
     if (!rg) return fail(OCEAN_E_INVALID_ARG, "null noise");
     char* dst = nullptr;
     if (int r = slice_ptr(ctx, OCEAN_TEX_NOISE, tile, 0, ctx->texels() * 8, &dst)) return r;
@@ -562,7 +594,7 @@ int ocean_set_noise(ocean_ctx* ctx, int tile, const float* rg) {
 }
 
 int ocean_generate_noise_device(ocean_ctx* ctx, uint64_t seed) {
-    if (int r = enter(ctx)) return r;
+    OCEAN_ENTER(ctx);
     const ocean::DevView v = ctx->view();
     OCEAN_HIP(ocean::launch_noise(v, seed, ctx->stream));
     OCEAN_HIP(hipStreamSynchronize(ctx->stream));
@@ -571,7 +603,7 @@ int ocean_generate_noise_device(ocean_ctx* ctx, uint64_t seed) {
 }
 
 int ocean_generate_noise(ocean_ctx* ctx, uint64_t seed) {
-    if (int r = enter(ctx)) return r;
+    OCEAN_ENTER(ctx);
     std::vector<float> host(ctx->texels() * 2);
     for (int t = 0; t < ctx->T; ++t) {
         ocean::generate_noise_host(ctx->n, seed + (uint64_t)t, host.data());
@@ -581,7 +613,7 @@ int ocean_generate_noise(ocean_ctx* ctx, uint64_t seed) {
 }
 
 int ocean_init_spectrum(ocean_ctx* ctx) {
-    if (int r = enter(ctx)) return r;
+    OCEAN_ENTER(ctx);
     if (!ctx->params_set) return fail(OCEAN_E_STATE, "ocean_set_params must precede ocean_init_spectrum");
     for (int t = 0; t < ctx->T; ++t)
         if (!ctx->noise_set[t]) return fail(OCEAN_E_STATE, "noise not set for tile " + std::to_string(t));
@@ -605,7 +637,7 @@ int ocean_init_spectrum(ocean_ctx* ctx) {
 }
 
 int ocean_reset_foam(ocean_ctx* ctx) {
-    if (int r = enter(ctx)) return r;
+    OCEAN_ENTER(ctx);
     if (ctx->turb) OCEAN_HIP(hipMemsetAsync(ctx->turb, 0, ctx->texels() * ctx->units() * 16, ctx->stream));
     if (ctx->foam) OCEAN_HIP(hipMemsetAsync(ctx->foam, 0, ctx->texels() * ctx->units() * 4, ctx->stream));
     if (ctx->turb_mips) OCEAN_HIP(hipMemsetAsync(ctx->turb_mips, 0, ctx->mip_chain * ctx->units() * 16, ctx->stream));
@@ -613,14 +645,14 @@ int ocean_reset_foam(ocean_ctx* ctx) {
 }
 
 int ocean_evolve(ocean_ctx* ctx, float time) {
-    if (int r = enter(ctx)) return r;
+    OCEAN_ENTER(ctx);
     if (!ctx->spectrum_ready) return fail(OCEAN_E_STATE, "ocean_init_spectrum must precede ocean_evolve");
     const ocean::DevView v = ctx->view();
     return timed(ctx, 2, [&] { return ocean::launch_evolve(v, time, ctx->stream); }, "evolve");
 }
 
 int ocean_ifft2d(ocean_ctx* ctx, int plane_mask) {
-    if (int r = enter(ctx)) return r;
+    OCEAN_ENTER(ctx);
     if (plane_mask < 0 || plane_mask > 15) return fail(OCEAN_E_INVALID_ARG, "plane_mask must be in [0, 15]");
     for (int p = 0; p < 4; ++p)
         if ((plane_mask & (1 << p)) && p >= ctx->P)
@@ -681,7 +713,7 @@ int ocean_ifft2d(ocean_ctx* ctx, int plane_mask) {
 }
 
 int ocean_fill(ocean_ctx* ctx) {
-    if (int r = enter(ctx)) return r;
+    OCEAN_ENTER(ctx);
     const ocean::DevView v = ctx->view();
     return timed(ctx, 2, [&] { return ocean::launch_fill(v, ctx->stream); }, "fill");
 }
@@ -699,7 +731,7 @@ int generate_mips(ocean_ctx* ctx) {
 }  // namespace
 
 int ocean_step(ocean_ctx* ctx, float time) {
-    if (int r = enter(ctx)) return r;
+    OCEAN_ENTER(ctx);
     if (!ctx->spectrum_ready) return fail(OCEAN_E_STATE, "ocean_init_spectrum must precede ocean_step");
     if (ctx->flags & OCEAN_F_UNFUSED) {
         if (int r = ocean_evolve(ctx, time)) return r;
@@ -839,7 +871,7 @@ int step_fused(ocean_ctx* ctx, float time) {
 }  // namespace
 
 int ocean_read(ocean_ctx* ctx, int texture, int tile, int cascade, void* dst, size_t bytes) {
-    if (int r = enter(ctx)) return r;
+    OCEAN_ENTER(ctx);
     if (!dst) return fail(OCEAN_E_INVALID_ARG, "null destination");
     char* src = nullptr;
     if (int r = slice_ptr(ctx, texture, tile, cascade, bytes, &src)) return r;
@@ -869,7 +901,7 @@ int mip_slice_ptr(ocean_ctx* ctx, int texture, int tile, int cascade, int level,
 
 int ocean_read_mip(ocean_ctx* ctx, int texture, int tile, int cascade, int level, void* dst, size_t bytes) {
     if (level == 0) return ocean_read(ctx, texture, tile, cascade, dst, bytes);
-    if (int r = enter(ctx)) return r;
+    OCEAN_ENTER(ctx);
     if (!dst) return fail(OCEAN_E_INVALID_ARG, "null destination");
     char* src = nullptr;
     size_t want = 0;
@@ -897,10 +929,17 @@ int ocean_get_mip_ptr(ocean_ctx* ctx, int texture, int level, void** ptr, size_t
 struct ocean_readback {
     hipEvent_t done = nullptr;   // the host copy has landed
     hipEvent_t after = nullptr;  // the snapshot is in the slot (the copy stream waits for it)
+    hipEvent_t start = nullptr;  // the copy stream reached the host copy (ocean_readback_copy_ms)
     int device = 0;
     void* slot = nullptr;
     std::shared_ptr<StagePool> pool;
 };
+
+namespace {
+// The host copy of ocean_read_async: hipMemcpyDeviceToHost (see docs/MEASUREMENTS.md section 8 for the
+// engine the runtime picks)
+constexpr hipMemcpyKind kReadbackCopyKind = hipMemcpyDeviceToHost;
+}  // namespace
 
 extern "C" {
 
@@ -908,7 +947,7 @@ int ocean_read_async(ocean_ctx* ctx, int texture, int tile, int cascade, void* d
                      ocean_readback** out) {
     if (!out) return fail(OCEAN_E_INVALID_ARG, "out is null");
     *out = nullptr;
-    if (int r = enter(ctx)) return r;
+    OCEAN_ENTER(ctx);
     if (!dst) return fail(OCEAN_E_INVALID_ARG, "null destination");
     char* src = nullptr;
     if (int r = slice_ptr(ctx, texture, tile, cascade, bytes, &src)) return r;
@@ -926,18 +965,21 @@ int ocean_read_async(ocean_ctx* ctx, int texture, int tile, int cascade, void* d
     // staging slot on the ctx stream (ordered after the queued steps and before later ones,
     // ~16 MiB at HBM speed), then the host copy on the copy stream, off the ctx stream's path.
     hipError_t e = hipEventCreateWithFlags(&rb->after, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&rb->done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreate(&rb->start);
+    if (e == hipSuccess) e = hipEventCreate(&rb->done);
     if (e == hipSuccess) e = rb->pool->take(&rb->slot);
     if (e == hipSuccess) e = hipMemcpyAsync(rb->slot, src, bytes, hipMemcpyDeviceToDevice, ctx->stream);
     if (e == hipSuccess) e = hipEventRecord(rb->after, ctx->stream);
     if (e == hipSuccess) e = hipStreamWaitEvent(ctx->copy_stream, rb->after, 0);
-    if (e == hipSuccess) e = hipMemcpyAsync(dst, rb->slot, bytes, hipMemcpyDeviceToHost, ctx->copy_stream);
+    if (e == hipSuccess) e = hipEventRecord(rb->start, ctx->copy_stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(dst, rb->slot, bytes, kReadbackCopyKind, ctx->copy_stream);
     if (e == hipSuccess) e = hipEventRecord(rb->done, ctx->copy_stream);
     if (e != hipSuccess) {
         (void)hipStreamSynchronize(ctx->copy_stream);
         (void)hipStreamSynchronize(ctx->stream);
         if (rb->slot) rb->pool->give(rb->slot);
         if (rb->done) (void)hipEventDestroy(rb->done);
+        if (rb->start) (void)hipEventDestroy(rb->start);
         if (rb->after) (void)hipEventDestroy(rb->after);
         delete rb;
         return hip_fail(e, "ocean_read_async");
@@ -962,15 +1004,24 @@ int ocean_readback_wait(ocean_readback* rb) {
 
 void ocean_readback_release(ocean_readback* rb) {
     if (!rb) return;
-    int prev = 0;
-    const bool had = hipGetDevice(&prev) == hipSuccess;
-    (void)hipSetDevice(rb->device);
-    (void)hipEventSynchronize(rb->done);  // the slot is free only once its host copy has landed
-    (void)hipEventDestroy(rb->done);
-    (void)hipEventDestroy(rb->after);
-    rb->pool->give(rb->slot);
+    {
+        DeviceScope device_scope(rb->device);
+        (void)hipEventSynchronize(rb->done);  // the slot is free only once its host copy has landed
+        (void)hipEventDestroy(rb->done);
+        (void)hipEventDestroy(rb->start);
+        (void)hipEventDestroy(rb->after);
+        rb->pool->give(rb->slot);
+    }
     delete rb;
-    if (had) (void)hipSetDevice(prev);  // the caller's current device is left as it was
+}
+
+int ocean_readback_copy_ms(ocean_readback* rb, float* ms) {
+    if (!rb || !ms) return fail(OCEAN_E_INVALID_ARG, "null readback or output");
+    const hipError_t q = hipEventQuery(rb->done);
+    if (q == hipErrorNotReady) return fail(OCEAN_E_STATE, "readback still pending");
+    if (q != hipSuccess) return hip_fail(q, "hipEventQuery");
+    OCEAN_HIP(hipEventElapsedTime(ms, rb->start, rb->done));
+    return OCEAN_OK;
 }
 
 int ocean_host_alloc(size_t bytes, void** out) {
@@ -986,7 +1037,7 @@ void ocean_host_free(void* p) {
 }
 
 int ocean_write(ocean_ctx* ctx, int texture, int tile, int cascade, const void* src, size_t bytes) {
-    if (int r = enter(ctx)) return r;
+    OCEAN_ENTER(ctx);
     if (!src) return fail(OCEAN_E_INVALID_ARG, "null source");
     if (texture == OCEAN_TEX_WAVES && !(ctx->flags & OCEAN_F_UNFUSED))
         return fail(OCEAN_E_UNSUPPORTED, "WAVES is read-only under the fused schedule (its row pass rebuilds the "
@@ -1027,13 +1078,13 @@ int ocean_get_stream(ocean_ctx* ctx, void** stream) {
 }
 
 int ocean_synchronize(ocean_ctx* ctx) {
-    if (int r = enter(ctx)) return r;
+    OCEAN_ENTER(ctx);
     OCEAN_HIP(hipStreamSynchronize(ctx->stream));
     return OCEAN_OK;
 }
 
+// (the caller has entered: OCEAN_ENTER)
 static int check_sample(ocean_ctx* ctx, int tile, const float* pts, int count, float* out) {
-    if (int r = enter(ctx)) return r;
     if (tile < 0 || tile >= ctx->T) return fail(OCEAN_E_INVALID_ARG, "tile out of range");
     if (count < 0) return fail(OCEAN_E_INVALID_ARG, "negative point count");
     if (count > 0 && (!pts || !out)) return fail(OCEAN_E_INVALID_ARG, "null points or output");
@@ -1043,6 +1094,7 @@ static int check_sample(ocean_ctx* ctx, int tile, const float* pts, int count, f
 }
 
 int ocean_sample_world_device(ocean_ctx* ctx, int tile, const float* points, int count, float* out) {
+    OCEAN_ENTER(ctx);
     if (int r = check_sample(ctx, tile, points, count, out)) return r;
     if (ctx->col_par >= 0) return fail(OCEAN_E_UNSUPPORTED, "world sampling of a column-parity shard (half the columns)");
     // k_sample_world reads floats and writes float4 rows (ocean.h)
@@ -1054,6 +1106,7 @@ int ocean_sample_world_device(ocean_ctx* ctx, int tile, const float* points, int
 }
 
 int ocean_sample_world(ocean_ctx* ctx, int tile, const float* points, int count, float* out) {
+    OCEAN_ENTER(ctx);
     if (int r = check_sample(ctx, tile, points, count, out)) return r;
     if (count == 0) return OCEAN_OK;
     const size_t in_bytes = (size_t)count * 3 * 4, out_bytes = (size_t)count * 12 * 4;
@@ -1076,7 +1129,7 @@ int ocean_sample_world(ocean_ctx* ctx, int tile, const float* points, int count,
 }
 
 int ocean_set_column_band(ocean_ctx* ctx, int x_begin, int x_count) {
-    if (int r = enter(ctx)) return r;
+    OCEAN_ENTER(ctx);
     const int n = ctx->n;
     const int g = std::min(n, std::max(16, 8192 / n));  // a multiple of every tile width of the fused passes
     if (x_begin < 0 || x_count < 1 || x_begin + x_count > n || x_begin % g || x_count % g)
@@ -1092,7 +1145,7 @@ int ocean_set_column_band(ocean_ctx* ctx, int x_begin, int x_count) {
 }
 
 int ocean_set_column_parity(ocean_ctx* ctx, int parity) {
-    if (int r = enter(ctx)) return r;
+    OCEAN_ENTER(ctx);
     if (parity < -1 || parity > 1) return fail(OCEAN_E_INVALID_ARG, "parity must be -1 (off), 0 or 1");
     if (parity < 0) {
         ctx->col_par = -1;
@@ -1104,11 +1157,17 @@ int ocean_set_column_parity(ocean_ctx* ctx, int parity) {
     if (ctx->flags & (OCEAN_F_UNFUSED | OCEAN_F_MIPS | OCEAN_F_DISPLACEMENT_ONLY))
         return fail(OCEAN_E_UNSUPPORTED, "a column parity needs the fused full-output schedule and no mip chains");
     if (!ctx->opt.q) return fail(OCEAN_E_UNSUPPORTED, "a column parity needs the three-plane frame (OCEAN_Q=0 is set)");
+    // pass A3PP reads h0(k) of mirror-pair rows from h0k (8 B per texel instead of h0's 16): allocated on
+    // the first parity, then kept up to date by ocean_init_spectrum (k_conjugate writes it)
     if (!ctx->h0k) {
-        // pass A3PP reads h0(k) of mirror-pair rows from h0k (8 B per texel instead of h0's 16): allocated on
-        // the first parity, then kept up to date by ocean_init_spectrum
         const size_t bytes = ctx->texels() * ctx->units() * 8;
         OCEAN_HIP(hipMalloc((void**)&ctx->h0k, bytes));
+        ctx->h0k_valid = false;
+    }
+    // extract whenever the spectrum exists (h0.zw = conj h0(-k)) and h0k does not match it yet: a failed
+    // extract leaves h0k_valid false, so the next call retries it; before ocean_init_spectrum there is
+    // nothing to extract, and the init fills h0k itself
+    if (!ctx->h0k_valid && ctx->h0_conj) {
         const ocean::DevView v = ctx->view();
         OCEAN_HIP(ocean::launch_h0k_extract(v, ctx->stream));
         OCEAN_HIP(hipStreamSynchronize(ctx->stream));
@@ -1121,7 +1180,7 @@ int ocean_set_column_parity(ocean_ctx* ctx, int parity) {
 }
 
 int ocean_set_kernel_timing(ocean_ctx* ctx, int enable) {
-    if (int r = enter(ctx)) return r;
+    OCEAN_ENTER(ctx);
     if (enable && ctx->event_pool.size() < 4096) {
         // pre-create events so the timed region never creates any
         while (ctx->event_pool.size() < 4096) {
@@ -1176,7 +1235,7 @@ int ocean_kernel_name(ocean_ctx* ctx, int kind, char* buf, size_t len) {
     if (kind < 0 || kind > 2) return fail(OCEAN_E_INVALID_ARG, "bad kind");
     buf[0] = 0;
     if (!ctx->kind_kernel[kind]) return fail(OCEAN_E_STATE, "no kernel of this kind launched yet");
-    if (int r = enter(ctx)) return r;
+    OCEAN_ENTER(ctx);
     const char* mangled = hipKernelNameRefByPtr(ctx->kind_kernel[kind], ctx->stream);
     if (!mangled) return fail(OCEAN_E_DEVICE, "hipKernelNameRefByPtr returned no name");
     int st = 0;
@@ -1188,7 +1247,7 @@ int ocean_kernel_name(ocean_ctx* ctx, int kind, char* buf, size_t len) {
 }
 
 int ocean_kernel_stats(ocean_ctx* ctx, int kind, double* total_ms, long long* launches) {
-    if (int r = enter(ctx)) return r;
+    OCEAN_ENTER(ctx);
     if (kind < 0 || kind > 2 || !total_ms || !launches) return fail(OCEAN_E_INVALID_ARG, "bad kind or null output");
     if (int r = fold_pending(ctx, true)) return r;
     *total_ms = ctx->kind_ms[kind];

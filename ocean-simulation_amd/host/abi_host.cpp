@@ -60,13 +60,19 @@ int main(int argc, char** argv) {
             for (auto& p : probe) heights.push_back(wb.GetWaterHeight(p[0], p[1]));
         }
         wb.WaitForReadbacks();
-        write_bin(out + "/buoyancy0.bin", wb.buoyancyData().data(), wb.buoyancyData().size());
+        {
+            const std::vector<float>& buoy = wb.buoyancyData();
+            write_bin(out + "/buoyancy0.bin", buoy.data(), buoy.size());
+        }
         write_bin(out + "/heights.bin", heights.data(), heights.size());
         wb.windSpeed = 12.0f;
         wb.OnValidate();
         wb.Update(0.5f);
         wb.WaitForReadbacks();
-        write_bin(out + "/buoyancy1.bin", wb.buoyancyData().data(), wb.buoyancyData().size());
+        {
+            const std::vector<float>& buoy = wb.buoyancyData();
+            write_bin(out + "/buoyancy1.bin", buoy.data(), buoy.size());
+        }
         std::vector<float> pts;
         for (int i = 0; i < 8; ++i) {
             pts.push_back(-300.0f + 97.5f * i);

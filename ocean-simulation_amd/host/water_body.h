@@ -146,10 +146,16 @@ public:
         ctx_ = nullptr;
     }
 
-    // The last landed displacement slice 0 (WaterBody.cs:295's array), a copy the caller owns as
-    // ToArray() gives; empty before the first readback lands.
-    std::vector<float> buoyancyData() const {
-        return held_ ? std::vector<float>(held_, held_ + SliceBytes() / 4) : std::vector<float>();
+    // The last landed displacement slice 0 (WaterBody.cs:295's array); empty before the first
+    // readback lands.  Copied out of its pinned slot once, on the first call after it lands; later
+    // calls return the same array until the next readback lands (the reference reads a field).
+    const std::vector<float>& buoyancyData() {
+        if (held_ && !buoy_valid_) {
+            buoy_.assign(held_, held_ + SliceBytes() / 4);
+            buoy_valid_ = true;
+        }
+        if (!held_) buoy_.clear();
+        return buoy_;
     }
     long requested() const { return requested_; }
     long completed() const { return completed_; }
@@ -165,6 +171,8 @@ private:
     const float* held_ = nullptr;  // the last landed slice, in its pinned slot (out of the ring)
     void* held_slot_ = nullptr;
     std::vector<float> last_;  // the last slice after OnDisable
+    std::vector<float> buoy_;  // buoyancyData's copy of the held slice
+    bool buoy_valid_ = false;
     long requested_ = 0, completed_ = 0;
 
     size_t SliceBytes() const { return (size_t)texturesSize * texturesSize * 16; }
@@ -189,6 +197,7 @@ private:
             if (held_slot_) free_.push_back(held_slot_);
             held_slot_ = p.buf;
             held_ = static_cast<const float*>(p.buf);
+            buoy_valid_ = false;
             ++completed_;
         } else {
             free_.push_back(p.buf);  // back to the ring

@@ -60,6 +60,7 @@ EXPORTED_SYMBOLS = (
     "ocean_write", "ocean_get_device_ptr", "ocean_get_stream", "ocean_synchronize",
     "ocean_set_kernel_timing", "ocean_kernel_stats", "ocean_step_bytes", "ocean_read_mip", "ocean_get_mip_ptr",
     "ocean_generate_noise_device", "ocean_read_async", "ocean_readback_status", "ocean_readback_wait", "ocean_readback_release",
+    "ocean_readback_copy_ms",
     "ocean_host_alloc", "ocean_host_free", "ocean_last_error", "ocean_abi_version", "ocean_set_column_band",
     "ocean_reset_foam", "ocean_sample_world", "ocean_sample_world_device", "ocean_kernel_name",
     "ocean_set_column_parity",
@@ -126,6 +127,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "ocean_readback_status": ([P], i),
         "ocean_readback_wait": ([P], i),
         "ocean_readback_release": ([P], None),
+        "ocean_readback_copy_ms": ([P, ctypes.POINTER(f)], i),
         "ocean_host_alloc": ([sz, ctypes.POINTER(P)], i),
         "ocean_host_free": ([P], None),
         "ocean_last_error": ([], ctypes.c_char_p),
@@ -370,6 +372,12 @@ class Readback:
     def wait(self) -> None:
         _check(self.lib.ocean_readback_wait(self._h), "ocean_readback_wait")
 
+    def copy_ms(self) -> float:
+        """The completed request's device-to-host copy duration (ocean_readback_copy_ms)."""
+        ms = ctypes.c_float()
+        _check(self.lib.ocean_readback_copy_ms(self._h, ctypes.byref(ms)), "ocean_readback_copy_ms")
+        return ms.value
+
     @property
     def data(self) -> np.ndarray:
         """A copy of the completed readback (waits if still pending)."""
@@ -451,6 +459,8 @@ class WaterBody:
         self._ring: List[PinnedBuffer] = []  # pinned readback slots, allocated in Awake
         self._idle: List[PinnedBuffer] = []
         self._held: Optional[PinnedBuffer] = None  # the pinned slot the last landed slice stays in
+        self._buoy_copy: Optional[np.ndarray] = None  # buoyancyData's copy of the landed slice (first access)
+        self.readback_copy_ms: Optional[List[float]] = None  # set to [] to log each landed copy's time
 
     def params(self) -> dict:
         return dict(wind_speed=self.windSpeed, wind_dir_x=self.windDirection[0], wind_dir_y=self.windDirection[1],
@@ -471,7 +481,7 @@ class WaterBody:
         self.ctx.init_spectrum()
         slice_bytes = self.texturesSize * self.texturesSize * 16
         # one slot more than the requests in flight: the one the last landed slice stays in
-        self._ring = [PinnedBuffer(slice_bytes) for _ in range(self.MAX_READBACKS_IN_FLIGHT + 1)]
+        self._ring = [PinnedBuffer(slice_bytes) for _ in range(self._in_flight() + 1)]
         self._idle = list(self._ring)
         self._held = None
         return self
@@ -491,6 +501,10 @@ class WaterBody:
     # 0.82 ms per frame, each copy stretched to 2.5x its time alone.
     MAX_READBACKS_IN_FLIGHT = 4
 
+    def _in_flight(self) -> int:
+        """The bound in force: at least one request (water_body.h clamps the same way)."""
+        return max(int(self.MAX_READBACKS_IN_FLIGHT), 1)
+
     def Update(self, time: float) -> None:
         """WaterBody.Update (WaterBody.cs:284-297): step, then issue a new AsyncGPUReadback
         request of displacement slice 0 EVERY frame (:288); requests complete in order and
@@ -499,7 +513,7 @@ class WaterBody:
         self._poll_readbacks()
         # at most MAX_READBACKS_IN_FLIGHT requests queued (the ring's extra slot holds the landed slice):
         # when full, wait for the oldest
-        while self._readbacks and (len(self._readbacks) >= self.MAX_READBACKS_IN_FLIGHT or not self._idle):
+        while self._readbacks and (len(self._readbacks) >= self._in_flight() or not self._idle):
             self._complete(self._readbacks.pop(0))
         slot = self._idle.pop()
         try:
@@ -516,18 +530,28 @@ class WaterBody:
         # buoyancyData copies it out only when a caller asks (16 MiB of host copy saved per frame
         # at 1024^2).
         view = rb.view()
+        if self.readback_copy_ms is not None:
+            self.readback_copy_ms.append(rb.copy_ms())
         slot = rb.slot
         rb.release()
         if self._held is not None:
             self._idle.append(self._held)
         self._held = slot
         self._buoy = view
+        self._buoy_copy = None
 
     @property
     def buoyancyData(self) -> Optional[np.ndarray]:
-        """The last landed displacement slice 0, [y][x][rgba] (WaterBody.cs:295's array): a copy the
-        caller owns, as ToArray() gives."""
-        return None if self._buoy is None else np.array(self._buoy)
+        """The last landed displacement slice 0, [y][x][rgba] (WaterBody.cs:295's array), read-only.
+        The slice is copied out of its pinned slot once, on the first access after it lands, and the
+        same array is returned until the next readback lands: per-sample indexing costs no copy, as
+        reading the reference's field does not."""
+        if self._buoy is None:
+            return None
+        if self._buoy_copy is None:
+            self._buoy_copy = np.array(self._buoy)
+            self._buoy_copy.flags.writeable = False
+        return self._buoy_copy
 
     def _poll_readbacks(self) -> None:
         while self._readbacks and self._readbacks[0].done():
@@ -573,7 +597,7 @@ class WaterBody:
             rb.release()
         self._readbacks = []
         if self._buoy is not None:  # the last landed slice outlives the pinned ring
-            self._buoy = np.array(self._buoy)
+            self._buoy = self.buoyancyData
         for b in self._ring:
             b.release()
         self._ring, self._idle, self._held = [], [], None

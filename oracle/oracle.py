@@ -396,3 +396,15 @@ def rel_err(a, b):
     b = np.asarray(b)
     den = np.abs(b).max()
     return float(np.abs(a - b).max() / (den if den > 0 else 1.0))
+
+
+def pointwise_err(a, b, frac=1e-3):
+    """SURVEY.md section 7's second tolerance clause: max |a-b| / |b| over the texels where
+    |b| >= frac * max|b| (the near-zero texels excluded).  Returns (error, texels in the mask)."""
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    mag = np.abs(b)
+    m = mag >= frac * mag.max() if mag.max() > 0 else np.zeros(b.shape, bool)
+    if not m.any():
+        return 0.0, 0
+    return float((np.abs(a[m] - b[m]) / mag[m]).max()), int(m.sum())

@@ -1,8 +1,8 @@
 """Host logic of bench.py's profile lookups (no GPU): roofline.traffic and the rocprofv3 figures are
 taken only from stamped records of the exact kernel symbol that ran and of the same config, preferring
 the record made with the loaded library (then with its sources, then the newest stamp), never by
-directory name; the builder's micro-benchmark ceilings only from this round's
-profiles/<ROUND>* directories, ROUND derived from the driver's BENCH records."""
+directory name; the builder's micro-benchmark ceilings from stamped records
+(ceilings.json), the current tool code's first, then the newest."""
 import json
 import os
 import sys
@@ -63,29 +63,41 @@ def test_record_exact_symbol_config_and_stamp(bench, tmp_path, monkeypatch):
     assert bench.find_record("cfg3", SYM_B3, str(tmp_path)) is None
 
 
-def test_round_is_derived(bench, tmp_path):
-    assert bench._current_round(str(tmp_path)) == "r01"
-    (tmp_path / "BENCH_r01.json").write_text("{}")
-    (tmp_path / "BENCH_r03.json").write_text("{}")
-    assert bench._current_round(str(tmp_path)) == "r04"
-    assert bench.ROUND == bench._current_round(ROOT)
+def _ceiling_rec(d, files, utc, tools=None):
+    os.makedirs(d, exist_ok=True)
+    for name, text in files.items():
+        (d / name).write_text(text)
+    if utc is not None:
+        json.dump({"kind": "ceilings", "utc": utc, "tool_code_sha256": tools or {}}, open(d / "ceilings.json", "w"))
 
 
-def test_ceilings_only_from_this_round(bench, tmp_path):
-    old = tmp_path / "r02x"
-    os.makedirs(old)
-    (old / "wrbench.txt").write_text("write nt 192 MiB         grid  2048     43.5 us   4632.1 GB/s\n")
-    (old / "aqbench.txt").write_text("AQ rows (y, N - y), half lines         17.2 us   7800.8 GB/s\n")
+def test_ceilings_by_stamp(bench, tmp_path):
+    """Micro-benchmark ceilings come from stamped records (ceilings.json), the current tool code's
+    first, then the newest stamp -- never from a directory name or the round."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import stamp as st
+    cur = {t: st.code_sha(os.path.join(ROOT, "tools", t)) for t in ("wrbench.hip", "aqbench.hip")}
+    aq = "AQ rows (y, N - y), half lines"
+    _ceiling_rec(tmp_path / "zz_unstamped", {"wrbench.txt": "write nt 192 MiB         grid  2048     43.5 us   4632.1 GB/s\n",
+                                             "aqbench.txt": aq + "         17.2 us   7800.8 GB/s\n"}, None)
     assert bench.write_ceilings(str(tmp_path)) is None
-    assert bench.shape_us("aqbench.txt", "AQ rows (y, N - y), half lines", str(tmp_path)) is None
-    cur = tmp_path / (bench.ROUND + "z")
-    os.makedirs(cur)
-    (cur / "wrbench.txt").write_text("write nt 192 MiB         grid  2048     44.0 us   4600.0 GB/s\n"
-                                     "write nt 1 GiB           grid  4096    263.9 us   4069.1 GB/s\n")
-    (cur / "aqbench.txt").write_text("AQ rows (y, N - y), half lines         17.0 us   7900.0 GB/s\n")
+    assert bench.shape_us("aqbench.txt", aq, str(tmp_path)) is None
+    _ceiling_rec(tmp_path / "r02_old", {"wrbench.txt": "write nt 192 MiB         grid  2048     44.0 us   4600.0 GB/s\n"
+                                                       "write nt 1 GiB           grid  4096    263.9 us   4069.1 GB/s\n",
+                                        "aqbench.txt": aq + "         17.0 us   7900.0 GB/s\n"},
+                 "2025-01-01T00:00:00Z", cur)
     wc = bench.write_ceilings(str(tmp_path))
     assert wc["nt_192MiB_GBs"] == 4600.0 and wc["nt_beyond_cache_GBs"] == 4069.1
-    assert bench.shape_us("aqbench.txt", "AQ rows (y, N - y), half lines", str(tmp_path))[0] == 17.0
+    assert wc["source"] == "profiles/r02_old/wrbench.txt"
+    assert bench.shape_us("aqbench.txt", aq, str(tmp_path))[0] == 17.0
+    # newer, same code: wins; newer still but another tool code: loses to the current code's record
+    _ceiling_rec(tmp_path / "aa_new", {"aqbench.txt": aq + "         16.5 us   8000.0 GB/s\n"}, "2025-06-01T00:00:00Z", cur)
+    _ceiling_rec(tmp_path / "bb_other_code", {"aqbench.txt": aq + "         15.0 us   9000.0 GB/s\n"},
+                 "2026-01-01T00:00:00Z", {"aqbench.hip": "0" * 64})
+    assert bench.shape_us("aqbench.txt", aq, str(tmp_path)) == (16.5, "profiles/aa_new/aqbench.txt")
+    # the committed tree quotes a stamped record
+    assert bench.write_ceilings() is not None
+    assert bench.shape_us("aqbench.txt", aq) is not None and bench.shape_us("bqbench.txt", "texture layout, nt") is not None
 
 
 def test_mip_record_per_frame(bench, tmp_path, monkeypatch):
@@ -118,3 +130,21 @@ def test_entry_record_sums_the_four_step_pair(bench, tmp_path, monkeypatch):
     assert r["avg_us"] == 55.0 and r["kernels"] == [SYM_BQ]
     _rec(tmp_path / "r04c5b", "cfg5", {c2: (1.0, 1)}, lib="LIB", utc="2027-01-01T00:00:00Z")  # C2 alone, newer
     assert bench.entry_record("cfg5", c2, str(tmp_path)) is None  # the pair's records sit in two directories
+
+
+def test_cfg1_line(bench):
+    """BASELINE configs[0] has a bench line: `bench.py --config cfg1` runs the scalar
+    CPU path at 256^2 x 1 with no GPU and prints one JSON line of the contract's keys, n_gpus 0, the
+    path labelled as the C port standing in for the C# one."""
+    import subprocess
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "cfg1", "--steps", "6",
+                          "--warmup", "2"], capture_output=True, text=True, timeout=300, check=True).stdout
+    lines = [ln for ln in out.splitlines() if ln.strip()]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "vs_baseline", "dtype", "data", "config", "path", "init_spectrum_ms"):
+        assert k in d, k
+    assert d["n_gpus"] == 0 and d["steps"] == 6 and d["unit"] == "frames/s" and d["value"] > 0
+    assert d["config"]["workload"].startswith("cfg1") and d["config"]["n"] == 256 and d["config"]["cascades"] == 1
+    assert d["path"]["kind"] == "port" and d["path"]["cores"] == 1 and "CpuOcean.cs" in d["path"]["what"]

@@ -24,7 +24,7 @@ def scene(n_cascades):
                  swell=c["swell"], fade=c["fade"]) for c in O.SCENE_CASCADES[:n_cascades]]
 
 
-@pytest.mark.parametrize("n,C,F", [(256, 3, 6), (1024, 4, 4), (1024, 1, 20)])  # 20 > the 8 requests the ring queues
+@pytest.mark.parametrize("n,C,F", [(256, 3, 6), (1024, 4, 4), (1024, 1, 20)])  # 20 > the 4 requests the ring queues
 def test_cpp_host_lifecycle(tmp_path, n, C, F):
     assert os.path.exists(HOST), "build it: make -C ocean-simulation_amd (or __graft_entry__.build())"
     env = dict(os.environ)

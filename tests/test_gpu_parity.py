@@ -875,6 +875,40 @@ def test_column_parity_shards_vs_oracle():
         ctx.close()
 
 
+def test_column_parity_call_orders():
+    """a column parity set BEFORE ocean_init_spectrum (h0k is allocated then, and filled by
+    the init), and an H0 upload on a parity context (the frame then refuses, E_STATE) followed by a
+    re-init, both give the oracle's columns b, b + 2, ... at 1e-5 (one 4096^2 cascade, two frames)."""
+    n, cas = 4096, O.SCENE_CASCADES[3:4]
+    noise = O.generate_noise(n, 20251121)
+    ctx = oh.OceanContext(n, 1, 1, 0)
+    ctx.set_params(O.scene_params(), cas)
+    ctx.set_noise(0, noise)
+    ctx.set_column_parity(1)
+    ctx.init_spectrum()
+    O.set_threads(min(16, os.cpu_count() or 1))
+    try:
+        oc = O.OracleOcean(n, O.scene_params(), cas, noise)
+
+        def check(t, what):
+            ctx.step(t)
+            disp, deriv, turb = oc.step(t)
+            for tex, ref in ((oh.TEX_DISP, disp[..., :3]), (oh.TEX_DERIV, deriv), (oh.TEX_TURB, turb)):
+                got = ctx.read(tex)[None, :, :n // 2, :ref.shape[-1]]
+                assert_channels(got, ref[:, :, 1::2], what=f"{what} tex {tex}")
+        check(0.5, "parity before init")
+        h0 = ctx.read(oh.TEX_H0)
+        ctx.write(oh.TEX_H0, h0)  # an upload: .zw may no longer be conj h0(-k) as far as the context knows
+        with pytest.raises(oh.OceanError) as e:
+            ctx.step(0.75)
+        assert e.value.code == oh.E_STATE
+        ctx.init_spectrum()  # the spectrum (and h0k) again from the parameters
+        check(1.0, "re-init after an H0 upload")
+    finally:
+        O.set_threads(1)
+        ctx.close()
+
+
 def test_column_parity_errors():
     ctx, _ = make_ctx(1024, O.SCENE_CASCADES[:1])
     with pytest.raises(oh.OceanError) as e:

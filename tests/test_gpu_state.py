@@ -102,3 +102,63 @@ def test_kernel_timing_events_bounded():
     ms_b, nb = ctx.kernel_stats(1)
     assert na == steps and nb == steps and ms_a > 0 and ms_b > 0
     ctx.close()
+
+
+def _hip_runtime():
+    """The process's HIP runtime (the copy torch loaded, which liboceanhip.so binds to), for
+    hipGetDevice / hipSetDevice."""
+    import ctypes
+    import torch
+    torch.cuda.init()
+    return ctypes.CDLL("libamdhip64.so.7", mode=ctypes.RTLD_GLOBAL | getattr(ctypes, "RTLD_NOLOAD", 4))
+
+
+def _current_device(hip):
+    import ctypes
+    d = ctypes.c_int(-1)
+    assert hip.hipGetDevice(ctypes.byref(d)) == 0
+    return d.value
+
+
+def test_caller_device_unchanged():
+    """Every call leaves the calling thread's current device as it found it (ocean.h, Conventions):
+    create, set_params, init, step, the async readback and its release, read, destroy.  On device 0
+    always; with a second device visible, a context on device 1 is driven while the caller sits on
+    device 0, and one on device 0 while the caller sits on device 1."""
+    import ctypes
+    import torch
+    hip = _hip_runtime()
+    n, cas = 128, O.SCENE_CASCADES[:2]
+
+    def lifecycle(dev):
+        ctx = oh.OceanContext(n, len(cas), 1, 0, device=dev)
+        yield ctx
+        ctx.set_params(O.scene_params(), cas)
+        yield ctx
+        ctx.generate_noise(20251121)
+        ctx.init_spectrum()
+        yield ctx
+        ctx.step(0.5)
+        yield ctx
+        dst = oh.PinnedBuffer(n * n * 16)
+        rb = ctx.read_async(oh.TEX_DISP, 0, 0, buf=dst)
+        yield ctx
+        rb.wait()
+        rb.release()
+        yield ctx
+        ctx.read(oh.TEX_DISP, 0, 0)
+        ctx.synchronize()
+        yield ctx
+        ctx.close()
+        dst.release()
+        yield None
+
+    pairs = [(0, 0)]
+    if torch.cuda.device_count() > 1:
+        pairs += [(0, 1), (1, 0)]
+    for caller, ctx_dev in pairs:
+        assert hip.hipSetDevice(ctypes.c_int(caller)) == 0
+        for step, _ in enumerate(lifecycle(ctx_dev)):
+            assert _current_device(hip) == caller, f"caller device moved after lifecycle step {step} " \
+                                                   f"(caller {caller}, context device {ctx_dev})"
+    assert hip.hipSetDevice(ctypes.c_int(0)) == 0

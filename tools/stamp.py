@@ -47,6 +47,35 @@ def stamp(config, command):
             "host": socket.gethostname(), "command": command}
 
 
+CEILING_TOOLS = {"wrbench.txt": "wrbench.hip", "aqbench.txt": "aqbench.hip", "bqbench.txt": "bqbench.hip"}
+
+
+def code_sha(path):
+    """sha256 of a micro-benchmark's code: its lines with // comments and blank lines dropped, so an
+    edit of a comment does not orphan the records the tool made."""
+    h = hashlib.sha256()
+    for line in open(path):
+        code = line.split("//", 1)[0].rstrip()
+        if code:
+            h.update(code.encode() + b"\n")
+    return h.hexdigest()
+
+
+def ceiling_stamp(utc=None, git_head=None):
+    """Identity of a directory of micro-benchmark records (wrbench / aqbench / bqbench .txt): the code
+    sha256 of each tool and when it ran.  bench.py quotes the newest record made by the current code
+    of the tool (then the newest at all), whatever the directory is called."""
+    tools = os.path.join(ROOT, "tools")
+    return {"kind": "ceilings",
+            "utc": utc or datetime.datetime.now(datetime.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ"),
+            "host": socket.gethostname(), "git_head": git_head,
+            "tool_code_sha256": {t: code_sha(os.path.join(tools, t)) for t in sorted(set(CEILING_TOOLS.values()))}}
+
+
 if __name__ == "__main__":
+    if sys.argv[1] == "--ceilings":  # stamp.py --ceilings <dir> [utc] [git_head]
+        d = sys.argv[2]
+        json.dump(ceiling_stamp(*(sys.argv[3:5])), open(os.path.join(d, "ceilings.json"), "w"), indent=1)
+        sys.exit(0)
     out, config, cmd = sys.argv[1], sys.argv[2], " ".join(sys.argv[3:])
     json.dump(stamp(config, cmd), open(out, "w"), indent=1)
