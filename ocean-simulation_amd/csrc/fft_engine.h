@@ -286,10 +286,11 @@ struct Engine {
     }
 
     // Stages ST.. from LDS; the last stage hands (m, q, value) to emit.  Butterflies of sequences
-    // b >= live are skipped (their lanes still join the stage barriers): an image with idle
+    // b >= live or b < lo are skipped (their lanes still join the stage barriers): an image with idle
     // sequence slots.
     template <int ST, class Emit>
-    static __device__ __forceinline__ void stages_from(float2* lds, const float2* tws, Emit& emit, int live = B) {
+    static __device__ __forceinline__ void stages_from(float2* lds, const float2* tws, Emit& emit, int live = B,
+                                                       int lo = 0) {
         constexpr int R = radix_of(N, ST, FIRST);
         constexpr int NS = ns_of(N, ST, FIRST);
         constexpr int BF = EL / R;
@@ -301,7 +302,7 @@ struct Engine {
         for (int m = 0; m < BF; ++m) {
             int b, j;
             bj<R>(lane() + m * THREADS, b, j);
-            if (b >= live) continue;
+            if (b >= live || b < lo) continue;
             if constexpr (linear()) {
                 const float2* src = lds + lidx(b, j);
 #pragma unroll
@@ -316,7 +317,7 @@ struct Engine {
         for (int m = 0; m < BF; ++m) {
             int b, j;
             bj<R>(lane() + m * THREADS, b, j);
-            if (b >= live) continue;
+            if (b >= live || b < lo) continue;
             TWT::template apply<ST>(&v[m * R], j, tws);
             Idft<R>::run(&v[m * R]);
             if constexpr (LAST) {
@@ -336,7 +337,7 @@ struct Engine {
         }
         if constexpr (!LAST) {
             stage_sync<ST>();
-            stages_from<ST + 1>(lds, tws, emit, live);
+            stages_from<ST + 1>(lds, tws, emit, live, lo);
         }
     }
 

@@ -100,12 +100,15 @@ __device__ __forceinline__ float2* q_side(const DevView& v, int u) { return v.qs
 // first and are not stored, except that item 0 carries srow in its second Q3 slot.  Lane j
 // evolves texels x = j + r N/4 of row y1 with their mirrors (N - x) % N in row y2 and holds
 // stage-0 butterfly j of row y1 and jm = (N/4 - j) % (N/4) of row y2.  LDS pass 0: Q1, Q2 of both
-// rows; pass 1: Q3 of both rows (two of its four sequence slots idle, their butterflies skipped).
+// rows; pass 1: Q3 of both rows in slots 2, 3 (slots 0, 1 idle, their butterflies skipped).
 // OFF32: the intermediate stores take a scalar unit base and a 32-bit lane offset (plane, row, tile,
 // column) instead of a 64-bit address (cfg3 pass A 29.15-29.40 -> 28.26-29.15 us); the host checks
 // that the chunk's three planes lie within 4 GiB of the base (go_aq), else the 64-bit form runs.
+// Three workgroups per CU (43.5 KiB of LDS each at N = 1024) need <= 168 VGPRs: the split pass 1 below
+// takes 170 unconstrained, 168 with two spilled.
 template <int N, bool BAND = false, int WT = 0, bool OFF32 = true>
-__global__ __launch_bounds__(N / 4) void k_pass_aq(DevView v, float time, int items) {
+__global__ __launch_bounds__(N / 4) __attribute__((amdgpu_waves_per_eu(N == 1024 ? 3 : 1, N == 1024 ? 3 : 10))) void
+k_pass_aq(DevView v, float time, int items) {
     constexpr int R0 = 4, NJ = N / R0;
     constexpr int IPU = N / 2 + 1;  // items per unit
     using TW = StageTw<N, R0>;
@@ -203,14 +206,22 @@ __global__ __launch_bounds__(N / 4) void k_pass_aq(DevView v, float time, int it
         }
 #pragma unroll
         for (int k = 0; k < 6; ++k) Idft<R0>::run(g[k]);
+        // SPLIT (N = 1024, wave-private stages): pass 1 (Q3 of both rows) runs on waves 2, 3 (slots 2, 3),
+        // and the barrier that closes it is the next item's first one, so waves 0, 1 evolve the next item
+        // meanwhile (cfg3 pass A 28.5-29.0 -> 27.4-28.0 us).  At N = 512 (two waves, stages with barriers)
+        // pass 1 stays in slots 0, 1 behind a closing barrier: the split form there is 1.8 % slower
+        // (docs/MEASUREMENTS.md section 8).
+        constexpr bool SPLIT = E::wave_private(1);
+        constexpr int Q3SLOT = SPLIT ? 2 : 0;
 #pragma unroll
         for (int ps = 0; ps < 2; ++ps) {
             if (ps == 0) {
+                if (SPLIT) __syncthreads();  // the previous item's pass 1 (waves 2, 3) has read slots 2, 3
 #pragma unroll
                 for (int k = 0; k < 4; ++k) put(k, (k & 1) ? jm : j, g[k]);
             } else {
-                put(0, j, g[4]);
-                put(1, y1 ? jm : j, g[5]);
+                put(Q3SLOT, j, g[4]);
+                put(Q3SLOT + 1, y1 ? jm : j, g[5]);
             }
             __syncthreads();
             auto emit = [&](int m, int q, float2 val) {
@@ -218,7 +229,7 @@ __global__ __launch_bounds__(N / 4) void k_pass_aq(DevView v, float time, int it
                 E::template bj<E::RL>((int)threadIdx.x + m * T, b, jj);
                 const int p = ps == 0 ? (b >> 1) : 2;
                 const int s = b & 1;
-                if (ps == 1 && b >= 2) return;  // idle slots
+                if (ps == 1 && (b >> 1) != (Q3SLOT >> 1)) return;  // idle slots
                 const int x = jj + q * NSL;
                 if (s && self) {  // self-mirror row: a duplicate, or row 0's srow
                     if (p == 2 && y1 == 0) q_side(v, u)[N + x] = val;
@@ -237,10 +248,10 @@ __global__ __launch_bounds__(N / 4) void k_pass_aq(DevView v, float time, int it
                     dst[(size_t)q * (NSL / W) * N * W] = val;
                 }
             };
-            // pass 1: sequence slots 2, 3 idle, their butterflies skipped (at N = 1024 the stages are
-            // wave-private, wave w = sequence w: waves 2, 3 skip them whole)
-            E::template stages_from<1>(lds, tws, emit, ps == 1 ? 2 : 4);
-            __syncthreads();
+            // pass 1: two sequence slots idle, their butterflies skipped (at N = 1024 the stages are
+            // wave-private, wave w = sequence w: waves 0, 1 skip them whole and go on to the next item)
+            E::template stages_from<1>(lds, tws, emit, ps == 1 ? Q3SLOT + 2 : 4, ps == 1 ? Q3SLOT : 0);
+            if (ps == 0 || !SPLIT) __syncthreads();
         }
 #pragma unroll
         for (int r = 0; r < R0; ++r) {

@@ -267,6 +267,70 @@ def test_frames_vs_oracle(n, ncasc, flags):
     ctx.close()
 
 
+# SURVEY.md section 7's second tolerance clause (pointwise 1e-5 where |b| >= 1e-3 max|b|) is infeasible for
+# the reference's own algorithm in fp32: on that mask the radix-2 fp32 oracle is 2.4e-4 .. 1.0e-2 away from
+# the float64 frame (tools/pointwise.py, profiles/r05_pointwise/pointwise.json).  The
+# replacement asserted here, per frame, cascade and output channel on the same mask: the library's pointwise
+# error against float64 is within PW_FACTOR of the oracle's own, and so is its pointwise distance to the
+# oracle.  Measured worst ratios: 2.5 / 2.9 (cfg2), 3.0 / 3.3 (cfg3), 2.2 / 2.1 (cfg5), the height channel
+# Dy in each (it shares its complex transform with Dyx, which is larger at short wavelengths).
+PW_FRAC = 1e-3
+PW_FACTOR = 4.0
+
+
+def _f64_frame(h0, waves, t, foam_prev, full):
+    """One cascade's frame in float64 (oracle.ref64's evolve, numpy ifft2, fill, foam) from the oracle's own
+    fp32 h0 / wave data: it differs from the oracle only in the per-frame arithmetic."""
+    P = [O.ref64.ifft2d(q) for q in O.ref64.evolve(h0.astype(np.float64), waves.astype(np.float64), t)[:4 if full else 2]]
+    out = {"disp": np.stack([P[0].real, P[1].real, P[0].imag], -1)}
+    foam = None
+    if full:
+        out["deriv"] = np.stack([P[2].real, P[2].imag, P[3].real, P[3].imag], -1)
+        jac = (1 + P[3].real) * (1 + P[3].imag) - P[1].imag ** 2
+        foam = (np.zeros_like(jac) if foam_prev is None else foam_prev) * float(O.FOAM_DECAY)
+        foam = np.where(foam < jac, foam + jac, foam)
+        out["turb"] = foam[..., None]
+    return out, foam
+
+
+@pytest.mark.parametrize("n,ncasc,flags,times", [(512, 1, oh.F_DISPLACEMENT_ONLY, (0.0, 1 / 60, 100.0)),
+                                                 (1024, 4, 0, (0.0, 1 / 60, 100.0)),
+                                                 (4096, 1, 0, (0.0, 1 / 60))])
+def test_pointwise_clause(n, ncasc, flags, times):
+    """SURVEY section 7 clause 2 as replaced (above): cfg2, cfg3 and one cfg5 cascade, frames with the foam
+    carried; clause 1 (1e-5 norm-relative against the oracle) is asserted beside it."""
+    full = not flags & oh.F_DISPLACEMENT_ONLY
+    cas = O.SCENE_CASCADES[4 - ncasc:] if n == 4096 else O.SCENE_CASCADES[:ncasc]
+    ctx, (noise,) = make_ctx(n, cas, flags=flags)
+    O.set_threads(oracle_threads() if n >= 2048 else 1)
+    try:
+        oc = O.OracleOcean(n, O.scene_params(), cas, noise, nplanes=4 if full else 2)
+        foam64 = [None] * ncasc
+        for t in times:
+            ctx.step(t)
+            disp, deriv, turb = oc.step(t)
+            got = {"disp": ctx.read_all(oh.TEX_DISP)[..., :3]}
+            ref = {"disp": disp[..., :3]}
+            if full:
+                got["deriv"], got["turb"] = ctx.read_all(oh.TEX_DERIV), ctx.read_all(oh.TEX_TURB)[..., :1]
+                ref["deriv"], ref["turb"] = deriv, turb[..., :1]
+            for c in range(ncasc):
+                exact, foam64[c] = _f64_frame(oc.h0[c], oc.waves[c], t, foam64[c], full)
+                for tex in got:
+                    for ch in range(got[tex].shape[-1]):
+                        a, b, x = got[tex][c, ..., ch], ref[tex][c, ..., ch], exact[tex][..., ch]
+                        what = f"t={t:g} cascade {c} {tex}.{'xyzw'[ch]}"
+                        assert O.rel_err(a, b) <= TOL, what
+                        own, _ = O.pointwise_err(b, x, PW_FRAC)
+                        mine, _ = O.pointwise_err(a, x, PW_FRAC)
+                        dist, _ = O.pointwise_err(a, b, PW_FRAC)
+                        assert mine <= PW_FACTOR * own, f"{what}: pointwise vs float64 {mine:.2e} > {PW_FACTOR} x {own:.2e}"
+                        assert dist <= PW_FACTOR * own, f"{what}: pointwise vs oracle {dist:.2e} > {PW_FACTOR} x {own:.2e}"
+    finally:
+        O.set_threads(1)
+        ctx.close()
+
+
 @pytest.mark.parametrize("n", [1024, 4096])
 def test_shallow_frames_vs_oracle(n):
     """Shallow water (depth 4, WaterBody.cs:14's default: the TMA correction's three branches

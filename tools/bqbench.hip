@@ -13,6 +13,9 @@
 //   5: as 4 with 16-B plane loads (k_bq_mem16; its two half-line stores per lane dominate)
 //   6: as 4 as flat contiguous streams (k_flat)
 //   7: as 6 with Q1 and Q2 interleaved into one 16-byte read stream (k_flat2)
+//   8: as 0's 80 B (foam state included) as flat contiguous streams (k_flat_foam): whole-line stores
+//      everywhere at pass BQ's own byte count, the bound a row-contiguous (column-first) pass B could reach
+//   9: as 0 with the foam state read back from TURB.x (a 16-B read) and no separate foam array (88 B)
 // Build: hipcc --offload-arch=gfx950 -O3 tools/bqbench.hip -o tools/bqbench
 #include <hip/hip_runtime.h>
 
@@ -84,6 +87,20 @@ __global__ void k_flat2(const f32x4* __restrict__ q12, const float2* __restrict_
     }
 }
 
+// 8: the bytes of 0 (planes, foam state read + write, three textures) as flat streams
+__global__ void k_flat_foam(const float2* __restrict__ tp, size_t ps, float* __restrict__ foam, f32x4* __restrict__ d0,
+                            f32x4* __restrict__ d1, f32x4* __restrict__ d2, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const float2 a = tp[i], b = tp[ps + i], c = tp[2 * ps + i];
+        const float f = foam[i] * 0.5f + c.x;
+        foam[i] = f;
+        const f32x4 v0 = {a.x, b.y, a.y, 1.0f}, v1 = {b.x, c.y, f, 1.0f}, v2 = {c.x, a.y, c.y, f};
+        __builtin_nontemporal_store(v0, d0 + i);
+        __builtin_nontemporal_store(v1, d1 + i);
+        __builtin_nontemporal_store(v2, d2 + i);
+    }
+}
+
 template <int MODE>
 __global__ __launch_bounds__(T) void k_bq_mem(const float2* __restrict__ tp, size_t ps, float* __restrict__ foam,
                                               f32x4* __restrict__ d0, f32x4* __restrict__ d1, f32x4* __restrict__ d2,
@@ -98,17 +115,22 @@ __global__ __launch_bounds__(T) void k_bq_mem(const float2* __restrict__ tp, siz
 #pragma unroll
             for (int i = 0; i < 16; ++i) v[p][i] = src[i * 64 * W];
         }
-        if (MODE != 4) {
+        float fs[16];
+        if (MODE == 9) {  // the foam state is TURB.x of the previous frame (d2 plays TURB)
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                fs[i] = d2[(size_t)u * N * N + (size_t)(lj + i * 64) * N + x0 + lb].x * 0.5f + v[2][i].x;
+        } else if (MODE != 4) {
             float* f = foam + (size_t)item * TILE + lj * W + lb;
 #pragma unroll
-            for (int i = 0; i < 16; ++i) f[i * 64 * W] = f[i * 64 * W] * 0.5f + v[2][i].x;
+            for (int i = 0; i < 16; ++i) f[i * 64 * W] = fs[i] = f[i * 64 * W] * 0.5f + v[2][i].x;
         }
 #pragma unroll
         for (int t = 0; t < 3; ++t) {
             f32x4* dst = t == 0 ? d0 : (t == 1 ? d1 : d2);
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                const f32x4 val = {v[t][i].x, v[(t + 1) % 3][i].y, v[t][i].y, 1.0f};
+                const f32x4 val = {MODE == 9 && t == 2 ? fs[i] : v[t][i].x, v[(t + 1) % 3][i].y, v[t][i].y, 1.0f};
                 size_t o;
                 if (MODE == 2) {
                     o = (size_t)item * TILE + (size_t)(lj + i * 64) * W + lb;
@@ -146,7 +168,7 @@ int main() {
     const double bytes_all = (double)tex * (24 + 8 + 48);
     for (int grid : {256, 512}) {
         printf("grid %d (%d workgroups of %d lanes per CU)\n", grid, grid / 256, T);
-        for (int mode = 0; mode < 8; ++mode) {
+        for (int mode = 0; mode < 10; ++mode) {
             auto run = [&]() {
                 if (mode == 0) hipLaunchKernelGGL(k_bq_mem<0>, dim3(grid), dim3(T), 0, 0, tp, tex, foam, d0, d1, d2, items);
                 if (mode == 1) hipLaunchKernelGGL(k_bq_mem<1>, dim3(grid), dim3(T), 0, 0, tp, tex, foam, d0, d1, d2, items);
@@ -156,6 +178,8 @@ int main() {
                 if (mode == 5)
                     hipLaunchKernelGGL(k_bq_mem16, dim3(grid), dim3(T), 0, 0, (const f32x4*)tp, tex / 2, d0, d1, d2, items);
                 if (mode == 6) hipLaunchKernelGGL(k_flat, dim3(grid * 8), dim3(256), 0, 0, tp, tex, d0, d1, d2, tex);
+                if (mode == 8) hipLaunchKernelGGL(k_flat_foam, dim3(grid * 8), dim3(256), 0, 0, tp, tex, foam, d0, d1, d2, tex);
+                if (mode == 9) hipLaunchKernelGGL(k_bq_mem<9>, dim3(grid), dim3(T), 0, 0, tp, tex, foam, d0, d1, d2, items);
                 if (mode == 7)
                     hipLaunchKernelGGL(k_flat2, dim3(grid * 8), dim3(256), 0, 0, (const f32x4*)tp, tp + 2 * tex, d0, d1, d2,
                                        tex);
@@ -172,8 +196,9 @@ int main() {
             const char* names[] = {"texture layout, nt", "texture layout, plain", "tile-major outputs, nt",
                                    "texture layout, waves sweep rows", "texture layout, nt, no foam (-8 B)",
                                    "no foam, 16-B plane loads", "no foam, flat streams (grid x 8 WGs)",
-                                   "no foam, flat, Q1|Q2 interleaved"};
-            const double bytes = mode >= 4 ? bytes_all * 72 / 80 : bytes_all;
+                                   "no foam, flat, Q1|Q2 interleaved", "flat streams with foam (80 B)",
+                                   "foam state from TURB.x (88 B)"};
+            const double bytes = (mode >= 4 && mode <= 7) ? bytes_all * 72 / 80 : (mode == 9 ? bytes_all * 88 / 80 : bytes_all);
             printf("%-34s %8.1f us %8.1f GB/s\n", names[mode], us, bytes / us / 1e3);
         }
     }
