@@ -163,10 +163,11 @@ struct OpSubTw {
 // k_rowsf: a one-row engine (N / 16 lanes); item n runs its rows n, n + L back to back with the next
 // row's loads in flight across each row's stages.  A lane's last-stage outputs sit at the same columns
 // x for both rows, so the fold is a radix-2 butterfly in registers as the second row's values are
-// emitted: z_0 = a0 + a1, z_1 = (a0 - a1) w_N^n.
+// emitted: z_0 = a0 + a1, z_1 = (a0 - a1) w_N^n.  In place (scratch == plane): an item writes only the
+// two rows it has read (z_0 to row n, z_1 to row n + L), after reading both.
 template <int N>
-__global__ __launch_bounds__(N / kElems) void k_rowsf(const float2* __restrict__ plane, float2* __restrict__ scratch,
-                                                      int items, const float2* __restrict__ tw) {
+__global__ __launch_bounds__(N / kElems) void k_rowsf(const float2* plane, float2* scratch, int items,
+                                                      const float2* __restrict__ tw) {
     constexpr int F = 2, L = N / F;
     using TW = StageTwLds<N>;
     using E = Engine<N, 1, false, true, 16, TW>;
@@ -275,6 +276,94 @@ __global__ __launch_bounds__(W * (N / F) / kElems) void k_colsf(const float2* __
     }
 }
 
+// The in-place column launch over the row launch's sub-planes (k_rowsf with scratch == plane: z_b at
+// rows b L + n of the plane itself).  Sub-plane b's outputs go to rows F m + b, which for m >= L/2 are
+// rows of sub-plane 1: so item = (unit-plane, W-column tile) transforms sub-plane 0 then sub-plane 1 of
+// its columns, writes sub-plane 0's outputs m < L/2 as they come (rows 2m < L, already read), holds the
+// other half (8 values per lane) in registers until every lane has read sub-plane 1's tile (the barrier
+// after its stage 0), then writes them.  No scratch: a chunk's cache footprint is its own planes, half of
+// k_colsf's.  Loads are issued into the stage-0 registers once their values are in the LDS image
+// (sub-plane 1 during sub-plane 0's stages, the next item's sub-plane 0 during sub-plane 1's), so no
+// second register buffer is needed for the prefetch.  G > 1 groups the 8-column halves of 16-column tiles
+// on one XCD as k_cols2 does.
+template <int N, int W, int G>
+__global__ __launch_bounds__(W * (N / 2) / kElems) void k_colsf_ip(float2* plane, int items,
+                                                                   const float2* __restrict__ tw) {
+    constexpr int F = 2, L = N / F;
+    using CT = ColTile<L, W>;  // geometry only: lanes, in_dy / out_dy
+    // W < 8: compact twiddles (6.6 instead of 18 KiB), so that two 4-column workgroups share a CU
+    using TW = std::conditional_t<(W < 8), StageTwCompactSub<L, N, 16>, OpSubTw<L, N>>;
+    using E = Engine<L, W, true, Engine<L, W, true, false>::seq_pad_ok(), 16, TW>;
+    static_assert(E::THREADS == CT::T && E::R0 == CT::R0 && E::RL == CT::RL, "tile geometry");
+    constexpr int T = E::THREADS;
+    constexpr int TILES = N / W;        // column tiles per unit-plane
+    constexpr int BF = kElems / E::RL;  // last-stage butterflies per lane
+    constexpr int HALF_Q = E::RL / 2;   // q >= HALF_Q: output m >= L/2 (out_dy's q stride is L / RL)
+    static_assert(CT::out_dy(0, HALF_Q) == L / 2 && (T / W) * BF <= L / E::RL, "held half = q >= RL / 2");
+    __shared__ float2 lds[E::LDS_ELEMS];
+    __shared__ float2 twl[TW::kLdsEntries];
+    TW::load(twl, tw, threadIdx.x, T);
+    const int lb = CT::lane_b(), lj = CT::lane_j();
+    const int voff = (lj * N + lb) * 8;      // input element (lb, n = lj) of a sub-plane tile
+    const int ooff = (F * lj * N + lb) * 8;  // output element (lb, y = F lj) of the tile's rows
+    auto tile_of = [&](int item) {
+        if constexpr (G > 1) return (item & ~(8 * G - 1)) + G * (item & 7) + ((item >> 3) & (G - 1));
+        else return item;
+    };
+    auto decode = [&](int item, int& up, int& x0) {
+        const int t = tile_of(item);
+        up = t / TILES;
+        x0 = (t - up * TILES) * W;
+    };
+    float2 cur[kElems];
+    float2 held[BF * (E::RL - HALF_Q)];  // sub-plane 0's outputs m >= L/2, sign applied
+    auto load = [&](int item, int b) {
+        int up, x0;
+        decode(item, up, x0);
+        const size_t o = (size_t)up * N * N + (size_t)b * L * N + x0;
+        const Win w = make_win(plane + o, (unsigned)(((size_t)L * N - x0) * 8));
+#pragma unroll
+        for (int i = 0; i < kElems; ++i) cur[i] = bload2(w, voff, CT::in_dy(i) * N * 8);
+    };
+    int item = blockIdx.x;
+    if (item < items) load(item, 0);
+    __syncthreads();  // twiddle table
+    for (; item < items; item += gridDim.x) {
+        int up, x0;
+        decode(item, up, x0);
+        const Win w = make_win(plane + (size_t)up * N * N + x0, 0);
+#pragma unroll
+        for (int b = 0; b < F; ++b) {
+#pragma unroll
+            for (int m = 0; m < kElems / E::R0; ++m) {
+                Idft<E::R0>::run(&cur[m * E::R0]);
+                E::stage0_store(lds, m, &cur[m * E::R0]);
+            }
+            __syncthreads();  // the image holds sub-plane b; every lane has read sub-plane b's tile
+            if (b == 0) {
+                load(item, 1);  // sub-plane 1, in flight across sub-plane 0's stages
+            } else {
+                if (item + (int)gridDim.x < items) load(item + gridDim.x, 0);  // the next item's sub-plane 0
+                // sub-plane 1 is read: sub-plane 0's outputs m >= L/2 may overwrite its rows now
+#pragma unroll
+                for (int m = 0; m < BF; ++m)
+#pragma unroll
+                    for (int q = HALF_Q; q < E::RL; ++q)
+                        gstore2(held[m * (E::RL - HALF_Q) + q - HALF_Q], w, ooff, F * CT::out_dy(m, q) * N * 8);
+            }
+            auto emit = [&](int m, int q, float2 val) {
+                const int dy = CT::out_dy(m, q);
+                const float s = perm_sign(x0 + lb, F * (lj + dy) + b);
+                const float2 o = make_float2(val.x * s, val.y * s);
+                if (b == 0 && q >= HALF_Q) held[m * (E::RL - HALF_Q) + q - HALF_Q] = o;
+                else gstore2(o, w, ooff + b * N * 8, F * dy * N * 8);
+            };
+            E::template stages_from<1>(lds, twl, emit);
+            __syncthreads();  // the image is free for the next stage 0
+        }
+    }
+}
+
 // --------------------------------------------------------------- launch
 template <class K>
 int persistent_grid(K kernel, int threads, int items) {
@@ -338,14 +427,27 @@ struct Cols2 {
 
 // Folded operator for N = 4096 over `ups` consecutive unit-planes: part 0 = k_rowsf (planes -> scratch
 // sub-planes), part 1 = k_colsf on XCD-paired 8-column halves (scratch -> planes, permuted).
+// scratch == nullptr: in place, part 0 = k_rowsf onto the planes themselves, part 1 = k_colsf_ip.
 struct OpFold {
     static constexpr int N = 4096, F = 2, W = 8, G = 2;
+#ifdef OP4K_W4
+    static constexpr int WIP = 4, GIP = 4;  // A/B build: 4-column tiles, four per 128-byte line on one XCD
+#else
+    static constexpr int WIP = W, GIP = G;
+#endif
     static hipError_t go(const DevView* v, float2* planes, int ups, float2* scratch, int part, hipStream_t s) {
         if (part == 0) {
             constexpr int T = N / kElems;
             const int items = ups * (N / F);
             const int g = persistent_grid(k_rowsf<N>, T, items);
-            launch((k_rowsf<N>), dim3(g), dim3(T), 0, s, (const float2*)planes, scratch, items, v->tw);
+            launch((k_rowsf<N>), dim3(g), dim3(T), 0, s, (const float2*)planes, scratch ? scratch : planes, items,
+                   v->tw);
+        } else if (!scratch) {
+            constexpr int T = WIP * (N / F) / kElems;
+            const int items = ups * (N / WIP);
+            int g = persistent_grid(k_colsf_ip<N, WIP, GIP>, T, items);
+            g -= g % (8 * GIP);  // the pieces of a tile on blocks b, b + 8, ... at every step of the item loop
+            launch((k_colsf_ip<N, WIP, GIP>), dim3(g), dim3(T), 0, s, planes, items, v->tw);
         } else {
             constexpr int T = W * (N / F) / kElems;
             const int items = ups * F * (N / W);

@@ -667,23 +667,21 @@ int ocean_ifft2d(ocean_ctx* ctx, int plane_mask) {
         int np = 1;  // run of consecutive planes: one launch per direction (planes are one allocation)
         while (p + np < 4 && (plane_mask & (1 << (p + np)))) ++np;
         if (ctx->n == 4096) {
-            // Folded columns (fft2.hip k_rowsf / k_colsf): per chunk of unit-planes, rows + the
-            // decimation-in-frequency fold -> scratch sub-planes, then 2048-point column tiles
-            // scratch -> planes; a chunk of at most OCEAN_OP_CHUNK_MIB stays in the Infinity Cache
-            // between the two launches (auto 128 MiB, one unit-plane: both launches are out of place, so
-            // a chunk occupies twice its size; 4 x 4096^2 x 4 planes, columns 256 / 128 MiB: 0.44 / 0.71)
+            // Folded columns, in place (fft2.hip k_rowsf / k_colsf_ip): per chunk of unit-planes, rows +
+            // the decimation-in-frequency fold onto the planes' own rows (z_b at rows b L + n), then
+            // 2048-point column tiles of both sub-planes per item, back into the planes, permuted.  A chunk
+            // of at most OCEAN_OP_CHUNK_MIB stays in the Infinity Cache between the two launches (auto 256
+            // MiB: two unit-planes; docs/MEASUREMENTS.md section 8).
             const int ups = np * (int)ctx->units();
-            const size_t scratch_ups = ctx->inter_units * ctx->P;
-            const long mib = ctx->opt.op_chunk_mib > 0 ? ctx->opt.op_chunk_mib : 128;
-            int k = (int)std::max<size_t>(1, ((size_t)mib << 20) / (up_elems * 8));
-            k = (int)std::min<size_t>((size_t)k, scratch_ups);
+            const long mib = ctx->opt.op_chunk_mib > 0 ? ctx->opt.op_chunk_mib : 256;
+            const int k = (int)std::max<size_t>(1, ((size_t)mib << 20) / (up_elems * 8));
             for (int c0 = 0; c0 < ups; c0 += k) {
                 const int kc = std::min(k, ups - c0);
                 float2* planes = ctx->plane[p] + (size_t)c0 * up_elems;
-                if (int r = timed(ctx, 0, [&] { return ocean::launch_ifft_fold(v, planes, kc, ctx->tplane, 0, ctx->stream); },
+                if (int r = timed(ctx, 0, [&] { return ocean::launch_ifft_fold(v, planes, kc, nullptr, 0, ctx->stream); },
                                   "ifft_rows"))
                     return r;
-                if (int r = timed(ctx, 1, [&] { return ocean::launch_ifft_fold(v, planes, kc, ctx->tplane, 1, ctx->stream); },
+                if (int r = timed(ctx, 1, [&] { return ocean::launch_ifft_fold(v, planes, kc, nullptr, 1, ctx->stream); },
                                   "ifft_cols"))
                     return r;
             }

@@ -131,11 +131,12 @@ def test_ifft2d_operator_large_vs_numpy(n, C, mask):
     ctx.close()
 
 
-@pytest.mark.parametrize("n,chunk_mib", [(2048, None), (2048, 64), (4096, None), (4096, 256)])
+@pytest.mark.parametrize("n,chunk_mib", [(2048, None), (2048, 64), (4096, None), (4096, 128), (4096, 768)])
 def test_ifft2d_operator_large_vs_oracle(n, chunk_mib, monkeypatch):
     """N = 2048 / 4096 operator against the reference's radix-2 schedule (oracle) on three planes of two
-    cascades (6 unit-planes): one chunk per unit-plane at 4096 by default (two at OCEAN_OP_CHUNK_MIB=256),
-    one chunk at 2048 by default (three at 64); plane 3 untouched."""
+    cascades (6 unit-planes): at 4096 in place, chunks of two unit-planes by default, one at
+    OCEAN_OP_CHUNK_MIB=128, all six in one chunk at 768; one chunk at 2048 by default (three at 64);
+    plane 3 untouched."""
     if chunk_mib:
         monkeypatch.setenv("OCEAN_OP_CHUNK_MIB", str(chunk_mib))
     C = 2

@@ -16,6 +16,9 @@
 //   8: as 0's 80 B (foam state included) as flat contiguous streams (k_flat_foam): whole-line stores
 //      everywhere at pass BQ's own byte count, the bound a row-contiguous (column-first) pass B could reach
 //   9: as 0 with the foam state read back from TURB.x (a 16-B read) and no separate foam array (88 B)
+//  10: as 0 with the foam state written by nontemporal stores
+//  11: as 0 with the foam loads issued first (before the plane loads) and the foam stores last
+//  12: as 0 with TURB carrying the new foam (the texture depends on the foam read, as in pass BQ)
 // Build: hipcc --offload-arch=gfx950 -O3 tools/bqbench.hip -o tools/bqbench
 #include <hip/hip_runtime.h>
 
@@ -109,6 +112,12 @@ __global__ __launch_bounds__(T) void k_bq_mem(const float2* __restrict__ tp, siz
     float2 v[3][16];
     for (int item = blockIdx.x; item < items; item += gridDim.x) {
         const int u = item / (N / W), x0 = (item % (N / W)) * W;
+        float fl[16];
+        float* fp = foam + (size_t)item * TILE + lj * W + lb;
+        if (MODE == 11) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) fl[i] = fp[i * 64 * W];
+        }
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
             const float2* src = tp + p * ps + (size_t)item * TILE + lj * W + lb;
@@ -120,17 +129,26 @@ __global__ __launch_bounds__(T) void k_bq_mem(const float2* __restrict__ tp, siz
 #pragma unroll
             for (int i = 0; i < 16; ++i)
                 fs[i] = d2[(size_t)u * N * N + (size_t)(lj + i * 64) * N + x0 + lb].x * 0.5f + v[2][i].x;
-        } else if (MODE != 4) {
-            float* f = foam + (size_t)item * TILE + lj * W + lb;
+        } else if (MODE == 10) {
 #pragma unroll
-            for (int i = 0; i < 16; ++i) f[i * 64 * W] = fs[i] = f[i * 64 * W] * 0.5f + v[2][i].x;
+            for (int i = 0; i < 16; ++i) {
+                fs[i] = fp[i * 64 * W] * 0.5f + v[2][i].x;
+                __builtin_nontemporal_store(fs[i], fp + i * 64 * W);
+            }
+        } else if (MODE == 11) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) fs[i] = fl[i] * 0.5f + v[2][i].x;
+        } else if (MODE != 4) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) fp[i * 64 * W] = fs[i] = fp[i * 64 * W] * 0.5f + v[2][i].x;
         }
 #pragma unroll
         for (int t = 0; t < 3; ++t) {
             f32x4* dst = t == 0 ? d0 : (t == 1 ? d1 : d2);
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                const f32x4 val = {MODE == 9 && t == 2 ? fs[i] : v[t][i].x, v[(t + 1) % 3][i].y, v[t][i].y, 1.0f};
+                const f32x4 val = {(MODE == 9 || MODE == 12) && t == 2 ? fs[i] : v[t][i].x, v[(t + 1) % 3][i].y,
+                                   v[t][i].y, 1.0f};
                 size_t o;
                 if (MODE == 2) {
                     o = (size_t)item * TILE + (size_t)(lj + i * 64) * W + lb;
@@ -144,6 +162,10 @@ __global__ __launch_bounds__(T) void k_bq_mem(const float2* __restrict__ tp, siz
                 if (MODE == 1) dst[o] = val;
                 else __builtin_nontemporal_store(val, dst + o);
             }
+        }
+        if (MODE == 11) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) fp[i * 64 * W] = fs[i];
         }
     }
 }
@@ -168,7 +190,7 @@ int main() {
     const double bytes_all = (double)tex * (24 + 8 + 48);
     for (int grid : {256, 512}) {
         printf("grid %d (%d workgroups of %d lanes per CU)\n", grid, grid / 256, T);
-        for (int mode = 0; mode < 10; ++mode) {
+        for (int mode = 0; mode < 13; ++mode) {
             auto run = [&]() {
                 if (mode == 0) hipLaunchKernelGGL(k_bq_mem<0>, dim3(grid), dim3(T), 0, 0, tp, tex, foam, d0, d1, d2, items);
                 if (mode == 1) hipLaunchKernelGGL(k_bq_mem<1>, dim3(grid), dim3(T), 0, 0, tp, tex, foam, d0, d1, d2, items);
@@ -180,6 +202,9 @@ int main() {
                 if (mode == 6) hipLaunchKernelGGL(k_flat, dim3(grid * 8), dim3(256), 0, 0, tp, tex, d0, d1, d2, tex);
                 if (mode == 8) hipLaunchKernelGGL(k_flat_foam, dim3(grid * 8), dim3(256), 0, 0, tp, tex, foam, d0, d1, d2, tex);
                 if (mode == 9) hipLaunchKernelGGL(k_bq_mem<9>, dim3(grid), dim3(T), 0, 0, tp, tex, foam, d0, d1, d2, items);
+                if (mode == 10) hipLaunchKernelGGL(k_bq_mem<10>, dim3(grid), dim3(T), 0, 0, tp, tex, foam, d0, d1, d2, items);
+                if (mode == 11) hipLaunchKernelGGL(k_bq_mem<11>, dim3(grid), dim3(T), 0, 0, tp, tex, foam, d0, d1, d2, items);
+                if (mode == 12) hipLaunchKernelGGL(k_bq_mem<12>, dim3(grid), dim3(T), 0, 0, tp, tex, foam, d0, d1, d2, items);
                 if (mode == 7)
                     hipLaunchKernelGGL(k_flat2, dim3(grid * 8), dim3(256), 0, 0, (const f32x4*)tp, tp + 2 * tex, d0, d1, d2,
                                        tex);
@@ -197,7 +222,8 @@ int main() {
                                    "texture layout, waves sweep rows", "texture layout, nt, no foam (-8 B)",
                                    "no foam, 16-B plane loads", "no foam, flat streams (grid x 8 WGs)",
                                    "no foam, flat, Q1|Q2 interleaved", "flat streams with foam (80 B)",
-                                   "foam state from TURB.x (88 B)"};
+                                   "foam state from TURB.x (88 B)", "foam stores nontemporal",
+                                   "foam loads first, stores last", "TURB carries the new foam"};
             const double bytes = (mode >= 4 && mode <= 7) ? bytes_all * 72 / 80 : (mode == 9 ? bytes_all * 88 / 80 : bytes_all);
             printf("%-34s %8.1f us %8.1f GB/s\n", names[mode], us, bytes / us / 1e3);
         }
