@@ -557,8 +557,8 @@ __global__ __launch_bounds__(N / 4) void k_pass_a3pp(DevView v, float time, int 
 //   step 2: R[Q4] -> (Dxz, Dzz)         kept (LDS)
 //   step 3: R[Q3] -> (Dyz, Dxx)         foam (Dxx, Dzz, Dxz), TURB, DERIV = (Dyx, Dyz, Dxx, Dzz)
 // Three tile loads per item run through a three-slot register ring (two steps ahead), as in
-// k_pass_b3; d0 is staged through LDS.
-template <int N, bool BAND = false, int WT = 0>
+// k_pass_b3; d0 is staged through LDS.  DC (DevView::disp_cached): DISP with default-policy stores.
+template <int N, bool BAND = false, int WT = 0, bool DC = false>
 __global__ __launch_bounds__((WT ? WT : b3_w(N)) * N / kElems) void k_pass_bq(DevView v, int items) {
     using CT = ColTile<N, WT ? WT : b3_w(N)>;
     using E = typename CT::E;
@@ -599,8 +599,12 @@ __global__ __launch_bounds__((WT ? WT : b3_w(N)) * N / kElems) void k_pass_bq(De
     };
     auto load = [&](int item, int p, float2 (&d)[kElems]) {
         const Win w = make_win(v.tplane + (size_t)p * v.inter_stride + (size_t)full(item) * TILE, TILE * 8);
+        // DC: the intermediate's loads are nontemporal too (it is dead once read), which leaves DISP the
+        // cache room; together +1.1-2.1 % at cfg3.  Without DC (chunked frames) they stay default-policy: at cfg4
+        // nontemporal loads measured -1.1 to +1.1 % on two boxes (docs/MEASUREMENTS.md section 8)
 #pragma unroll
-        for (int i = 0; i < kElems; ++i) d[i] = bload2(w, toff * 8, CT::in_dy(i) * W * 8);
+        for (int i = 0; i < kElems; ++i)
+            d[i] = DC ? bload2<2>(w, toff * 8, CT::in_dy(i) * W * 8) : bload2(w, toff * 8, CT::in_dy(i) * W * 8);
     };
 
     float2 cur[kElems], nxt[kElems], nx2[kElems], dd[DPL], srow = make_float2(0.0f, 0.0f);
@@ -659,7 +663,8 @@ __global__ __launch_bounds__((WT ? WT : b3_w(N)) * N / kElems) void k_pass_bq(De
                     kput(i, make_float2(re, im));
                 } else if (st == 1) {  // (Dx, Dz): DISP
                     const float2 k = kget(i);
-                    gstore4_nt(make_float4(re, k.x, im, 1.0f), wd, voff16, so);
+                    if constexpr (DC) gstore4(make_float4(re, k.x, im, 1.0f), wd, voff16, so);
+                    else gstore4_nt(make_float4(re, k.x, im, 1.0f), wd, voff16, so);
                     kreg[i] = k.y;
                 } else if (st == 2) {  // (Dxz, Dzz)
                     kput(i, make_float2(re, im));
@@ -733,19 +738,22 @@ hipError_t go_a3q(const DevView& v, float t, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <int N, bool BAND = false, int WT = 0>
+template <int N, bool BAND = false, int WT = 0, bool DC = false>
 hipError_t go_bq(const DevView& v, hipStream_t s) {
     if constexpr (WT == 0) {
-        if (v.tile_w != inter_w(N)) return go_bq<N, BAND, 4>(v, s);
+        if (v.tile_w != inter_w(N)) return go_bq<N, BAND, 4, DC>(v, s);
     }
     if constexpr (!BAND) {
-        if (v.nx != N) return go_bq<N, true, WT>(v, s);
+        if (v.nx != N) return go_bq<N, true, WT, DC>(v, s);
+    }
+    if constexpr (!DC) {
+        if (v.disp_cached) return go_bq<N, BAND, WT, true>(v, s);
     }
     constexpr int W = WT ? WT : b3_w(N);
     constexpr int T = W * N / kElems;
     const int items = v.units * (v.nx / W);
-    const int g = grid_q(k_pass_bq<N, BAND, WT>, T, items);
-    launch((k_pass_bq<N, BAND, WT>), dim3(g), dim3(T), 0, s, v, items);
+    const int g = grid_q(k_pass_bq<N, BAND, WT, DC>, T, items);
+    launch((k_pass_bq<N, BAND, WT, DC>), dim3(g), dim3(T), 0, s, v, items);
     return hipGetLastError();
 }
 

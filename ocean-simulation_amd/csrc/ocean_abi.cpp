@@ -802,6 +802,20 @@ bool use_q(const ocean_ctx* ctx) {
     return ctx->n >= 2048 || (ctx->opt.a4 && ctx->h0k_valid);  // N <= 1024: the mirror-pair row pass reads h0k
 }
 
+// Pass BQ may write DISP with default-policy stores (DevView::disp_cached) when the whole frame is one chunk
+// and its cache-resident set -- h0k, the three-plane intermediate, the foam state -- plus DISP fits 224 MiB of
+// the 256 MiB Infinity Cache: DISP then waits there and is written back while the next pass A runs, when HBM
+// has headroom.  cfg3 (4 x 1024^2, 208 MiB): 11.83-11.88 -> 12.08-12.11 k frames/s; a cfg4 chunk (32 units of
+// 512^2, 288 MiB) lost 7.5 % the same way, and DISP + TURB at cfg3 lost 7 % (docs/MEASUREMENTS.md section 8).
+bool disp_fits_cache(const ocean_ctx* ctx, bool q, int chunk) {
+#ifdef OCEAN_AB_NO_DISP_CACHE  // A/B builds only (make VARIANT=... EXTRA=-DOCEAN_AB_NO_DISP_CACHE)
+    return false;
+#endif
+    if (!q || ctx->n > 1024 || chunk < (int)ctx->units()) return false;
+    const size_t bytes = ctx->texels() * ctx->units() * (8 + 24 + 4 + 16);
+    return bytes <= ((size_t)224 << 20);
+}
+
 int step_fused(ocean_ctx* ctx, float time) {
     // pass A: mirror-pair rows (N = 512, 1024 with 4 planes and h0k valid) or per-texel
     // rows; pass B: column tiles (N <= 1024) or the four-step column passes (N >= 2048)
@@ -811,6 +825,7 @@ int step_fused(ocean_ctx* ctx, float time) {
     if (ctx->col_par >= 0 && !q)
         return fail(OCEAN_E_STATE, "a column parity needs the three-plane frame (h0 from ocean_init_spectrum)");
     const int U = (int)ctx->units(), K = std::min(chunk_units(ctx, q ? q_planes(ctx) : ctx->P), (int)ctx->inter_units);
+    v.disp_cached = disp_fits_cache(ctx, q, K);
     for (int u0 = 0; u0 < U; u0 += K) {
         const ocean::DevView c = (K >= U) ? v : sub_view(v, u0, std::min(K, U - u0), ctx->inter_units < ctx->units());
         if (q && ctx->n >= 2048) {

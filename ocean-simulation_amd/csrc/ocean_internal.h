@@ -78,6 +78,10 @@ struct DevView {
     // column parity (ocean_set_column_parity): the context computes the columns x = xstr * m + xpar and
     // stores column x at texture / intermediate column m < N / xstr; xstr = 1, xpar = 0 when off
     int xstr, xpar;
+    // pass BQ writes DISP with default-policy stores instead of nontemporal ones: the slice stays in the
+    // Infinity Cache and is written back while the next pass A runs, when HBM has headroom.  Set by the host
+    // where the frame's re-read set plus DISP fits the cache (ocean_abi.cpp disp_fits_cache).
+    bool disp_cached;
 };
 
 struct SpectrumParams {
