@@ -38,6 +38,7 @@ from ocean_hip.shard import plan_shard, reduce_timing, tile_seed  # noqa: E402
 
 PREWARM_S = 0.5  # device clock ramp before the warm-up steps (see main)
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md (chip-level parameters)
+HBM_COPY_GBS = 6290.0  # the same guide's measured float4 copy rate; SURVEY.md 8d asks for both fractions
 
 SCENE_PARAMS = dict(wind_speed=8.0, wind_dir_x=1.0, wind_dir_y=-1.0, gravity=9.81, fetch=50000.0, depth=2560.0)
 SCENE_CASCADES = [  # Assets/Scenes/Waves.unity (+ unreferenced 4th cascade :1572-1576)
@@ -296,6 +297,7 @@ def ifft_measure(ctx, reps, record_config):
             "achieved_GBs": round(fft_bytes / (kern_us * 1e-6) / 1e9, 1),
             "frac": round(fft_bytes / (kern_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
             "wall_frac": round(fft_bytes / (stage_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+            "wall_frac_of_measured_copy": round(fft_bytes / (stage_us * 1e-6) / 1e9 / HBM_COPY_GBS, 4),
             "symbols": syms, "rocprof": rocprof, "traffic": traffic}
 
 
@@ -791,6 +793,7 @@ def main():
                                       f"over {world} GPU(s), no collective"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "measured_copy_GBs": HBM_COPY_GBS, "frac_of_measured_copy": round(achieved / HBM_COPY_GBS, 4),
                          "traffic": traffic,  # HBM bytes per launch (PMC), like `achieved`
                          "traffic_per_step": int(traffic * launches_per_step) if traffic else None,
                          "traffic_source": record["dir"] if record else None,
@@ -808,6 +811,7 @@ def main():
             "frame": {"algorithmic_bytes_per_gpu": B["frame"],
                       "achieved_GBs_per_gpu": round(B["frame"] / (elapsed / args.steps) / 1e9, 1),
                       "frac_per_gpu": round(B["frame"] / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
+                      "frac_of_measured_copy_per_gpu": round(B["frame"] / (elapsed / args.steps) / 1e9 / HBM_COPY_GBS, 4),
                       "ms_per_step_with_kernel_events": round(1e3 * elapsed_ev / args.steps, 5)},
             "ifft_stage": ifft_stage,
             "cache": cache,
