@@ -19,6 +19,8 @@
 //  10: as 0 with the foam state written by nontemporal stores
 //  11: as 0 with the foam loads issued first (before the plane loads) and the foam stores last
 //  12: as 0 with TURB carrying the new foam (the texture depends on the foam read, as in pass BQ)
+//  13: as 12 with the first texture (DISP) written by default-policy stores and the plane loads nontemporal:
+//      pass BQ's DC form (the frame's re-read set plus DISP in the Infinity Cache)
 // Build: hipcc --offload-arch=gfx950 -O3 tools/bqbench.hip -o tools/bqbench
 #include <hip/hip_runtime.h>
 
@@ -122,7 +124,15 @@ __global__ __launch_bounds__(T) void k_bq_mem(const float2* __restrict__ tp, siz
         for (int p = 0; p < 3; ++p) {
             const float2* src = tp + p * ps + (size_t)item * TILE + lj * W + lb;
 #pragma unroll
-            for (int i = 0; i < 16; ++i) v[p][i] = src[i * 64 * W];
+            for (int i = 0; i < 16; ++i) {
+                if (MODE == 13) {
+                    typedef float f32x2 __attribute__((ext_vector_type(2)));
+                    const f32x2 x = __builtin_nontemporal_load(reinterpret_cast<const f32x2*>(src + i * 64 * W));
+                    v[p][i] = make_float2(x.x, x.y);
+                } else {
+                    v[p][i] = src[i * 64 * W];
+                }
+            }
         }
         float fs[16];
         if (MODE == 9) {  // the foam state is TURB.x of the previous frame (d2 plays TURB)
@@ -147,7 +157,7 @@ __global__ __launch_bounds__(T) void k_bq_mem(const float2* __restrict__ tp, siz
             f32x4* dst = t == 0 ? d0 : (t == 1 ? d1 : d2);
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                const f32x4 val = {(MODE == 9 || MODE == 12) && t == 2 ? fs[i] : v[t][i].x, v[(t + 1) % 3][i].y,
+                const f32x4 val = {(MODE == 9 || MODE >= 12) && t == 2 ? fs[i] : v[t][i].x, v[(t + 1) % 3][i].y,
                                    v[t][i].y, 1.0f};
                 size_t o;
                 if (MODE == 2) {
@@ -159,7 +169,7 @@ __global__ __launch_bounds__(T) void k_bq_mem(const float2* __restrict__ tp, siz
                 } else {
                     o = (size_t)u * N * N + (size_t)(lj + i * 64) * N + x0 + lb;
                 }
-                if (MODE == 1) dst[o] = val;
+                if (MODE == 1 || (MODE == 13 && t == 0)) dst[o] = val;
                 else __builtin_nontemporal_store(val, dst + o);
             }
         }
@@ -190,7 +200,7 @@ int main() {
     const double bytes_all = (double)tex * (24 + 8 + 48);
     for (int grid : {256, 512}) {
         printf("grid %d (%d workgroups of %d lanes per CU)\n", grid, grid / 256, T);
-        for (int mode = 0; mode < 13; ++mode) {
+        for (int mode = 0; mode < 14; ++mode) {
             auto run = [&]() {
                 if (mode == 0) hipLaunchKernelGGL(k_bq_mem<0>, dim3(grid), dim3(T), 0, 0, tp, tex, foam, d0, d1, d2, items);
                 if (mode == 1) hipLaunchKernelGGL(k_bq_mem<1>, dim3(grid), dim3(T), 0, 0, tp, tex, foam, d0, d1, d2, items);
@@ -205,6 +215,7 @@ int main() {
                 if (mode == 10) hipLaunchKernelGGL(k_bq_mem<10>, dim3(grid), dim3(T), 0, 0, tp, tex, foam, d0, d1, d2, items);
                 if (mode == 11) hipLaunchKernelGGL(k_bq_mem<11>, dim3(grid), dim3(T), 0, 0, tp, tex, foam, d0, d1, d2, items);
                 if (mode == 12) hipLaunchKernelGGL(k_bq_mem<12>, dim3(grid), dim3(T), 0, 0, tp, tex, foam, d0, d1, d2, items);
+                if (mode == 13) hipLaunchKernelGGL(k_bq_mem<13>, dim3(grid), dim3(T), 0, 0, tp, tex, foam, d0, d1, d2, items);
                 if (mode == 7)
                     hipLaunchKernelGGL(k_flat2, dim3(grid * 8), dim3(256), 0, 0, (const f32x4*)tp, tp + 2 * tex, d0, d1, d2,
                                        tex);
@@ -223,7 +234,8 @@ int main() {
                                    "no foam, 16-B plane loads", "no foam, flat streams (grid x 8 WGs)",
                                    "no foam, flat, Q1|Q2 interleaved", "flat streams with foam (80 B)",
                                    "foam state from TURB.x (88 B)", "foam stores nontemporal",
-                                   "foam loads first, stores last", "TURB carries the new foam"};
+                                   "foam loads first, stores last", "TURB carries the new foam",
+                                   "as 12, DISP cached, nt plane loads"};
             const double bytes = (mode >= 4 && mode <= 7) ? bytes_all * 72 / 80 : (mode == 9 ? bytes_all * 88 / 80 : bytes_all);
             printf("%-34s %8.1f us %8.1f GB/s\n", names[mode], us, bytes / us / 1e3);
         }
