@@ -105,9 +105,10 @@ def test_ifft2d_operator_vs_oracle(n):
 @pytest.mark.parametrize("n,C,mask", [(2048, 1, 0b0001), (4096, 4, 0b1111), (4096, 1, 0b0110), (4096, 2, 0b1001)])
 def test_ifft2d_operator_large_vs_numpy(n, C, mask):
     """The operator at N = 2048 / 4096 on every requested plane of every cascade, against numpy's
-    float64 ifft2 (ref64); 4 x 4096^2 x 4 planes is cfg5's whole plane set (2 GiB).  At 4096: rows +
-    decimation-in-frequency fold into the scratch, then 2048-point column tiles (fft2.hip k_rowsf /
-    k_colsf); at 2048 in-place rows, then XCD-paired 8-column halves of whole columns (Cols2)."""
+    float64 ifft2 (ref64); 4 x 4096^2 x 4 planes is cfg5's whole plane set (2 GiB).  At 4096, in place: rows
+    + the decimation-in-frequency fold onto their own rows, then both 2048-point sub-planes of a column
+    tile per workgroup (fft2.hip k_rowsf / k_colsf_ip); at 2048 in-place rows, then XCD-paired 8-column
+    halves of whole columns (Cols2)."""
     ctx = oh.OceanContext(n, C, 1)
     planes = [p for p in range(4) if mask >> p & 1]
 
@@ -787,6 +788,8 @@ def test_async_readback_matches_read():
     for c in range(len(cas)):
         got = reqs[c].data
         assert reqs[c].done()
+        # the copy's own duration (ocean_readback_copy_ms): a 1 MiB device-to-host copy, well under a second
+        assert 0.0 < reqs[c].copy_ms() < 1000.0
         reqs[c].release()
         ref = make_ctx(n, cas)[0]
         ref.step(0.5)
