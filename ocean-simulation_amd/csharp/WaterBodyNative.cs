@@ -32,6 +32,9 @@ namespace OceanHip
 
         public void Awake()
         {
+            // the rules this facade relies on (ocean.h: ABI 3, no call moves the caller's current device)
+            if (OceanNative.ocean_abi_version() != 3)
+                throw new InvalidOperationException("liboceanhip ABI " + OceanNative.ocean_abi_version() + ", expected 3");
             OceanNative.Check(OceanNative.ocean_create(device, texturesSize, cascades.Length, 1, OceanFlags.Mips, out ctx),
                               "ocean_create");
             ApplyParams();
