@@ -18,7 +18,11 @@ import ocean_hip as oh  # noqa: E402
 frames = int(sys.argv[1]) if len(sys.argv) > 1 else 200
 wb = oh.scene_water_body(n=1024, n_cascades=4, seed=20251121).Awake()
 ctx = wb.ctx
-slot = wb._ring[0]
+# the probe's own pinned slots (borrowing the facade's ring capped the deepest ring at its 5 slots
+# and could reuse the slot the facade's landed slice sits in)
+SLOT_BYTES = 1024 * 1024 * 16
+slots = [oh.PinnedBuffer(SLOT_BYTES) for _ in range(8)]
+slot = slots[0]
 for f in range(20):
     ctx.step(f / 60.0)
 ctx.synchronize()
@@ -55,7 +59,7 @@ out["host_copy_GBs"] = round(16 * 2**20 / (out["host_copy_out_16MiB_ms"] * 1e-3)
 out["update_loop_ms"] = timed(lambda f: wb.Update(f / 60.0))
 wb.WaitForReadback()
 # the readback ring alone (no frames): 8 requests in flight, the oldest waited when the ring is full
-ring, idle = [], list(wb._ring)
+ring, idle = [], list(slots)
 
 
 def ring_only(f):
@@ -75,7 +79,8 @@ for r in ring:
 
 
 def ring_loop(depth, with_step, k=frames):
-    idle_slots, q = list(wb._ring[:depth]), []
+    assert depth <= len(slots)
+    idle_slots, q = list(slots[:depth]), []
 
     def finish(r):
         r.wait()
@@ -108,4 +113,6 @@ t_issue = (time.perf_counter() - t0) / frames * 1e3
 ctx.synchronize()
 out["host_issue_step_ms"] = t_issue
 wb.OnDisable()
+for b in slots:
+    b.release()
 print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in out.items()}))
