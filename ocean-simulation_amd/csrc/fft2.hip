@@ -430,11 +430,7 @@ struct Cols2 {
 // scratch == nullptr: in place, part 0 = k_rowsf onto the planes themselves, part 1 = k_colsf_ip.
 struct OpFold {
     static constexpr int N = 4096, F = 2, W = 8, G = 2;
-#ifdef OP4K_W4
-    static constexpr int WIP = 4, GIP = 4;  // A/B build: 4-column tiles, four per 128-byte line on one XCD
-#else
-    static constexpr int WIP = W, GIP = G;
-#endif
+    static constexpr int WIP = W, GIP = G;  // the in-place column tiles (4-column tiles: 0.48, log section 8)
     static hipError_t go(const DevView* v, float2* planes, int ups, float2* scratch, int part, hipStream_t s) {
         if (part == 0) {
             constexpr int T = N / kElems;

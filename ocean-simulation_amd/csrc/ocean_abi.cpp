@@ -808,9 +808,6 @@ bool use_q(const ocean_ctx* ctx) {
 // has headroom.  cfg3 (4 x 1024^2, 208 MiB): 11.83-11.88 -> 12.08-12.11 k frames/s; a cfg4 chunk (32 units of
 // 512^2, 288 MiB) lost 7.5 % the same way, and DISP + TURB at cfg3 lost 7 % (docs/MEASUREMENTS.md section 8).
 bool disp_fits_cache(const ocean_ctx* ctx, bool q, int chunk) {
-#ifdef OCEAN_AB_NO_DISP_CACHE  // A/B builds only (make VARIANT=... EXTRA=-DOCEAN_AB_NO_DISP_CACHE)
-    return false;
-#endif
     if (!q || ctx->n > 1024 || chunk < (int)ctx->units()) return false;
     const size_t bytes = ctx->texels() * ctx->units() * (8 + 24 + 4 + 16);
     return bytes <= ((size_t)224 << 20);
