@@ -21,6 +21,8 @@
 //  12: as 0 with TURB carrying the new foam (the texture depends on the foam read, as in pass BQ)
 //  13: as 12 with the first texture (DISP) written by default-policy stores and the plane loads nontemporal:
 //      pass BQ's DC form (the frame's re-read set plus DISP in the Infinity Cache)
+//  14: as 12 with the foam state lane-major (each lane's 16 values contiguous: 4 float4 loads and stores
+//      instead of 16 + 16 dword accesses)
 // Build: hipcc --offload-arch=gfx950 -O3 tools/bqbench.hip -o tools/bqbench
 #include <hip/hip_runtime.h>
 
@@ -135,7 +137,18 @@ __global__ __launch_bounds__(T) void k_bq_mem(const float2* __restrict__ tp, siz
             }
         }
         float fs[16];
-        if (MODE == 9) {  // the foam state is TURB.x of the previous frame (d2 plays TURB)
+        if (MODE == 14) {
+            const int lane = lj * W + lb;
+            const f32x4* f4 = reinterpret_cast<const f32x4*>(foam + (size_t)item * TILE) + lane * 4;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const f32x4 x = f4[k];
+                fs[4 * k] = x.x * 0.5f + v[2][4 * k].x;
+                fs[4 * k + 1] = x.y * 0.5f + v[2][4 * k + 1].x;
+                fs[4 * k + 2] = x.z * 0.5f + v[2][4 * k + 2].x;
+                fs[4 * k + 3] = x.w * 0.5f + v[2][4 * k + 3].x;
+            }
+        } else if (MODE == 9) {  // the foam state is TURB.x of the previous frame (d2 plays TURB)
 #pragma unroll
             for (int i = 0; i < 16; ++i)
                 fs[i] = d2[(size_t)u * N * N + (size_t)(lj + i * 64) * N + x0 + lb].x * 0.5f + v[2][i].x;
@@ -177,6 +190,14 @@ __global__ __launch_bounds__(T) void k_bq_mem(const float2* __restrict__ tp, siz
 #pragma unroll
             for (int i = 0; i < 16; ++i) fp[i * 64 * W] = fs[i];
         }
+        if (MODE == 14) {
+            f32x4* f4 = reinterpret_cast<f32x4*>(foam + (size_t)item * TILE) + (lj * W + lb) * 4;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const f32x4 x = {fs[4 * k], fs[4 * k + 1], fs[4 * k + 2], fs[4 * k + 3]};
+                f4[k] = x;
+            }
+        }
     }
 }
 
@@ -200,7 +221,7 @@ int main() {
     const double bytes_all = (double)tex * (24 + 8 + 48);
     for (int grid : {256, 512}) {
         printf("grid %d (%d workgroups of %d lanes per CU)\n", grid, grid / 256, T);
-        for (int mode = 0; mode < 14; ++mode) {
+        for (int mode = 0; mode < 15; ++mode) {
             auto run = [&]() {
                 if (mode == 0) hipLaunchKernelGGL(k_bq_mem<0>, dim3(grid), dim3(T), 0, 0, tp, tex, foam, d0, d1, d2, items);
                 if (mode == 1) hipLaunchKernelGGL(k_bq_mem<1>, dim3(grid), dim3(T), 0, 0, tp, tex, foam, d0, d1, d2, items);
@@ -216,6 +237,7 @@ int main() {
                 if (mode == 11) hipLaunchKernelGGL(k_bq_mem<11>, dim3(grid), dim3(T), 0, 0, tp, tex, foam, d0, d1, d2, items);
                 if (mode == 12) hipLaunchKernelGGL(k_bq_mem<12>, dim3(grid), dim3(T), 0, 0, tp, tex, foam, d0, d1, d2, items);
                 if (mode == 13) hipLaunchKernelGGL(k_bq_mem<13>, dim3(grid), dim3(T), 0, 0, tp, tex, foam, d0, d1, d2, items);
+                if (mode == 14) hipLaunchKernelGGL(k_bq_mem<14>, dim3(grid), dim3(T), 0, 0, tp, tex, foam, d0, d1, d2, items);
                 if (mode == 7)
                     hipLaunchKernelGGL(k_flat2, dim3(grid * 8), dim3(256), 0, 0, (const f32x4*)tp, tp + 2 * tex, d0, d1, d2,
                                        tex);
@@ -235,7 +257,7 @@ int main() {
                                    "no foam, flat, Q1|Q2 interleaved", "flat streams with foam (80 B)",
                                    "foam state from TURB.x (88 B)", "foam stores nontemporal",
                                    "foam loads first, stores last", "TURB carries the new foam",
-                                   "as 12, DISP cached, nt plane loads"};
+                                   "as 12, DISP cached, nt plane loads", "as 12, foam lane-major (float4)"};
             const double bytes = (mode >= 4 && mode <= 7) ? bytes_all * 72 / 80 : (mode == 9 ? bytes_all * 88 / 80 : bytes_all);
             printf("%-34s %8.1f us %8.1f GB/s\n", names[mode], us, bytes / us / 1e3);
         }
