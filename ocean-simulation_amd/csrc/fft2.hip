@@ -285,7 +285,10 @@ __global__ __launch_bounds__(W * (N / F) / kElems) void k_colsf(const float2* __
 // k_colsf's.  Loads are issued into the stage-0 registers once their values are in the LDS image
 // (sub-plane 1 during sub-plane 0's stages, the next item's sub-plane 0 during sub-plane 1's), so no
 // second register buffer is needed for the prefetch.  G > 1 groups the 8-column halves of 16-column tiles
-// on one XCD as k_cols2 does.
+// on one XCD as k_cols2 does.  The outputs stored as they come (three quarters) are nontemporal, the held
+// quarter default-policy: the next chunk's row launch then reads its planes past a cache that the
+// finished chunk's outputs do not fill (rows 0.71 -> 0.77, columns unchanged at 0.65, wall 0.68 -> 0.70;
+// all nontemporal: columns 0.62, wall 0.69; docs/MEASUREMENTS.md section 8).
 template <int N, int W, int G>
 __global__ __launch_bounds__(W * (N / 2) / kElems) void k_colsf_ip(float2* plane, int items,
                                                                    const float2* __restrict__ tw) {
@@ -356,7 +359,7 @@ __global__ __launch_bounds__(W * (N / 2) / kElems) void k_colsf_ip(float2* plane
                 const float s = perm_sign(x0 + lb, F * (lj + dy) + b);
                 const float2 o = make_float2(val.x * s, val.y * s);
                 if (b == 0 && q >= HALF_Q) held[m * (E::RL - HALF_Q) + q - HALF_Q] = o;
-                else gstore2(o, w, ooff + b * N * 8, F * dy * N * 8);
+                else gstore2_nt(o, w, ooff + b * N * 8, F * dy * N * 8);
             };
             E::template stages_from<1>(lds, twl, emit);
             __syncthreads();  // the image is free for the next stage 0

@@ -63,6 +63,11 @@ __device__ __forceinline__ void gstore4_nt(float4 x, const Win& w, int voff, int
     const f32x4 v = {x.x, x.y, x.z, x.w};
     __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(w.p + (store_off_t)(voff + soff)));
 }
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void gstore2_nt(float2 x, const Win& w, int voff, int soff) {
+    const f32x2 v = {x.x, x.y};
+    __builtin_nontemporal_store(v, reinterpret_cast<f32x2*>(w.p + (store_off_t)(voff + soff)));
+}
 __device__ __forceinline__ void store4_nt(float4* p, float4 x) {
     const f32x4 v = {x.x, x.y, x.z, x.w};
     __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
