@@ -222,7 +222,9 @@ __global__ __launch_bounds__(kSeq * kL1 / kElems) void k_col4s2(DevView v, int i
                     } else {  // (Dyz, Dxx): foam, TURB, DERIV, NORMAL
                         const float2 k = kget(i);
                         const float f = foam_update(fb[i], im, k.y, k.x);
-                        foam[(size_t)L0 * dy * kWT] = f;
+                        // the foam state (256 MiB at cfg5) is read back only next frame: nontemporal
+                        // (cfg5 447-448 -> 450-451 frames/s; cfg3 / cfg4 keep theirs cached, log section 8)
+                        __builtin_nontemporal_store(f, &foam[(size_t)L0 * dy * kWT]);
                         store4_nt(turb + to, make_float4(f, f, f, f));
                         store4_nt(deriv + to, make_float4(kreg[i], re, im, k.y));
                         if (v.normals) store4_nt(nrm + to, normal_from_deriv(kreg[i], re, im, k.y));
