@@ -154,20 +154,21 @@ struct OpSubTw {
 // ------------------------------------------------- folded columns (N = 4096)
 // The column transform at N = F L (F = 2) split by decimation in frequency:
 //   X[F m + b] = sum_{n < L} z_b[n] w_L^(n m),   z_b[n] = w_N^(n b) (a[n] + (-1)^b a[n + L]).
-// k_rowsf transforms rows n and n + L of one unit-plane, folds the two results column by column into
-// z_b[n] and stores z_b at row b L + n of the scratch (sub-plane b); k_colsf runs L-point column tiles
-// over the scratch's sub-planes -- the N = 2048 column shape (8-column halves, XCD-paired: 64-byte
-// pieces of 128-byte lines) -- and writes row F m + b of the plane, permuted.  The 4-column tiles of a
-// whole 4096-point column (32-byte pieces, 0.57 of peak) are not needed (docs/MEASUREMENTS.md section 3).
+// Both launches work in place on the planes.  k_rowsf transforms rows n and n + L of one unit-plane,
+// folds the two results column by column into z_b[n] and stores z_b at row b L + n (sub-plane b);
+// k_colsf_ip runs L-point column tiles over both sub-planes -- the N = 2048 column shape (8-column
+// halves, XCD-paired: 64-byte pieces of 128-byte lines) -- and writes row F m + b, permuted.  The
+// 4-column tiles of a whole 4096-point column (32-byte pieces, 0.57 of peak) are not needed, and the
+// round-4 form through a scratch plane set (twice the cache footprint per chunk) is gone
+// (docs/MEASUREMENTS.md sections 3 and 8).
 
 // k_rowsf: a one-row engine (N / 16 lanes); item n runs its rows n, n + L back to back with the next
 // row's loads in flight across each row's stages.  A lane's last-stage outputs sit at the same columns
 // x for both rows, so the fold is a radix-2 butterfly in registers as the second row's values are
-// emitted: z_0 = a0 + a1, z_1 = (a0 - a1) w_N^n.  In place (scratch == plane): an item writes only the
-// two rows it has read (z_0 to row n, z_1 to row n + L), after reading both.
+// emitted: z_0 = a0 + a1, z_1 = (a0 - a1) w_N^n.  An item writes only the two rows it has read (z_0 to
+// row n, z_1 to row n + L), after reading both.
 template <int N>
-__global__ __launch_bounds__(N / kElems) void k_rowsf(const float2* plane, float2* scratch, int items,
-                                                      const float2* __restrict__ tw) {
+__global__ __launch_bounds__(N / kElems) void k_rowsf(float2* plane, int items, const float2* __restrict__ tw) {
     constexpr int F = 2, L = N / F;
     using TW = StageTwLds<N>;
     using E = Engine<N, 1, false, true, 16, TW>;
@@ -190,7 +191,7 @@ __global__ __launch_bounds__(N / kElems) void k_rowsf(const float2* plane, float
     __syncthreads();  // twiddle table
     for (; it < items; it += gridDim.x) {
         const int up = it / L, n = it - up * L;
-        float2* dst = scratch + (size_t)up * N * N + (size_t)n * N;  // row b L + n holds z_b
+        float2* dst = plane + (size_t)up * N * N + (size_t)n * N;  // row b L + n holds z_b
         const float2 wf = tw[n];                                      // w_N^n
 #pragma unroll
         for (int k = 0; k < F; ++k) {
@@ -216,79 +217,19 @@ __global__ __launch_bounds__(N / kElems) void k_rowsf(const float2* plane, float
     }
 }
 
-// item = (unit-plane, sub-plane b, W-column tile); G > 1 groups the pieces of 16-column tiles on one
-// XCD as k_cols2 does.
-template <int N, int F, int W, int G>
-__global__ __launch_bounds__(W * (N / F) / kElems) void k_colsf(const float2* __restrict__ scratch,
-                                                                float2* __restrict__ plane, int items,
-                                                                const float2* __restrict__ tw) {
-    constexpr int L = N / F;
-    using CT = ColTile<L, W>;  // geometry only: lanes, in_dy / out_dy
-    using TW = OpSubTw<L, N>;
-    using E = Engine<L, W, true, Engine<L, W, true, false>::seq_pad_ok(), 16, TW>;
-    static_assert(E::THREADS == CT::T && E::R0 == CT::R0 && E::RL == CT::RL, "tile geometry");
-    constexpr int T = E::THREADS;
-    constexpr int TILES = N / W;  // column tiles per sub-plane
-    __shared__ float2 lds[E::LDS_ELEMS];
-    __shared__ float2 twl[TW::kLdsEntries];
-    TW::load(twl, tw, threadIdx.x, T);
-    const int lb = CT::lane_b(), lj = CT::lane_j();
-    const int voff = (lj * N + lb) * 8;          // input element (lb, n = lj) of a sub-plane tile
-    const int ooff = (F * lj * N + lb) * 8;      // output element (lb, y = F lj) from the tile's row b
-    auto tile_of = [&](int item) {
-        if constexpr (G > 1) return (item & ~(8 * G - 1)) + G * (item & 7) + ((item >> 3) & (G - 1));
-        else return item;
-    };
-    auto decode = [&](int item, int& up, int& b, int& x0) {
-        const int t = tile_of(item);
-        up = t / (F * TILES);
-        const int r = t - up * F * TILES;
-        b = r / TILES;
-        x0 = (r - b * TILES) * W;
-    };
-    float2 cur[kElems], nxt[kElems];
-    auto load = [&](int item, float2 (&d)[kElems]) {
-        int up, b, x0;
-        decode(item, up, b, x0);
-        const size_t o = (size_t)up * N * N + (size_t)b * L * N + x0;
-        const Win w = make_win(scratch + o, (unsigned)(((size_t)L * N - x0) * 8));
-#pragma unroll
-        for (int i = 0; i < kElems; ++i) d[i] = bload2(w, voff, CT::in_dy(i) * N * 8);
-    };
-    int item = blockIdx.x;
-    if (item < items) load(item, cur);
-    __syncthreads();
-    for (; item < items; item += gridDim.x) {
-        const int next = item + gridDim.x;
-        if (next < items) load(next, nxt);
-        int up, b, x0;
-        decode(item, up, b, x0);
-        const Win w = make_win(plane + (size_t)up * N * N + (size_t)b * N + x0, 0);
-        auto emit = [&](int m, int q, float2 val) {
-            const int dy = CT::out_dy(m, q);
-            const float s = perm_sign(x0 + lb, F * (lj + dy) + b);
-            gstore2(make_float2(val.x * s, val.y * s), w, ooff, F * dy * N * 8);
-        };
-        E::run_regs(cur, lds, twl, emit);
-#pragma unroll
-        for (int i = 0; i < kElems; ++i) cur[i] = nxt[i];
-        __syncthreads();
-    }
-}
-
-// The in-place column launch over the row launch's sub-planes (k_rowsf with scratch == plane: z_b at
-// rows b L + n of the plane itself).  Sub-plane b's outputs go to rows F m + b, which for m >= L/2 are
-// rows of sub-plane 1: so item = (unit-plane, W-column tile) transforms sub-plane 0 then sub-plane 1 of
-// its columns, writes sub-plane 0's outputs m < L/2 as they come (rows 2m < L, already read), holds the
-// other half (8 values per lane) in registers until every lane has read sub-plane 1's tile (the barrier
-// after its stage 0), then writes them.  No scratch: a chunk's cache footprint is its own planes, half of
-// k_colsf's.  Loads are issued into the stage-0 registers once their values are in the LDS image
-// (sub-plane 1 during sub-plane 0's stages, the next item's sub-plane 0 during sub-plane 1's), so no
-// second register buffer is needed for the prefetch.  G > 1 groups the 8-column halves of 16-column tiles
-// on one XCD as k_cols2 does.  The outputs stored as they come (three quarters) are nontemporal, the held
-// quarter default-policy: the next chunk's row launch then reads its planes past a cache that the
-// finished chunk's outputs do not fill (rows 0.71 -> 0.77, columns unchanged at 0.65, wall 0.68 -> 0.70;
-// all nontemporal: columns 0.62, wall 0.69; docs/MEASUREMENTS.md section 8).
+// The in-place column launch over the row launch's sub-planes (k_rowsf: z_b at rows b L + n of the plane
+// itself).  Sub-plane b's outputs go to rows F m + b, which for m >= L/2 are rows of sub-plane 1: so item =
+// (unit-plane, W-column tile) transforms sub-plane 0 then sub-plane 1 of its columns, writes sub-plane 0's
+// outputs m < L/2 as they come (rows 2m < L, already read), holds the other half (8 values per lane) in
+// registers until every lane has read sub-plane 1's tile (the barrier after its stage 0), then writes
+// them.  A chunk's cache footprint is its own planes.  Loads are issued into the stage-0 registers once
+// their values are in the LDS image (sub-plane 1 during sub-plane 0's stages, the next item's sub-plane 0
+// during sub-plane 1's), so no second register buffer is needed for the prefetch.  G > 1 groups the
+// 8-column halves of 16-column tiles on one XCD as k_cols2 does.  The outputs stored as they come (three
+// quarters) are nontemporal, the held quarter default-policy: the next chunk's row launch then reads its
+// planes past a cache that the finished chunk's outputs do not fill (rows 0.71 -> 0.77, columns
+// unchanged at 0.65, wall 0.68 -> 0.70; all nontemporal: columns 0.62, wall 0.69; docs/MEASUREMENTS.md
+// section 8).
 template <int N, int W, int G>
 __global__ __launch_bounds__(W * (N / 2) / kElems) void k_colsf_ip(float2* plane, int items,
                                                                    const float2* __restrict__ tw) {
@@ -428,31 +369,22 @@ struct Cols2 {
     }
 };
 
-// Folded operator for N = 4096 over `ups` consecutive unit-planes: part 0 = k_rowsf (planes -> scratch
-// sub-planes), part 1 = k_colsf on XCD-paired 8-column halves (scratch -> planes, permuted).
-// scratch == nullptr: in place, part 0 = k_rowsf onto the planes themselves, part 1 = k_colsf_ip.
+// Folded operator for N = 4096 over `ups` consecutive unit-planes, in place: part 0 = k_rowsf (rows + fold
+// onto the planes' own rows), part 1 = k_colsf_ip (both sub-planes of an 8-column tile per item, permuted).
 struct OpFold {
-    static constexpr int N = 4096, F = 2, W = 8, G = 2;
-    static constexpr int WIP = W, GIP = G;  // the in-place column tiles (4-column tiles: 0.48, log section 8)
-    static hipError_t go(const DevView* v, float2* planes, int ups, float2* scratch, int part, hipStream_t s) {
+    static constexpr int N = 4096, F = 2, W = 8, G = 2;  // 4-column tiles: 0.48 (docs/MEASUREMENTS.md section 8)
+    static hipError_t go(const DevView* v, float2* planes, int ups, int part, hipStream_t s) {
         if (part == 0) {
             constexpr int T = N / kElems;
             const int items = ups * (N / F);
             const int g = persistent_grid(k_rowsf<N>, T, items);
-            launch((k_rowsf<N>), dim3(g), dim3(T), 0, s, (const float2*)planes, scratch ? scratch : planes, items,
-                   v->tw);
-        } else if (!scratch) {
-            constexpr int T = WIP * (N / F) / kElems;
-            const int items = ups * (N / WIP);
-            int g = persistent_grid(k_colsf_ip<N, WIP, GIP>, T, items);
-            g -= g % (8 * GIP);  // the pieces of a tile on blocks b, b + 8, ... at every step of the item loop
-            launch((k_colsf_ip<N, WIP, GIP>), dim3(g), dim3(T), 0, s, planes, items, v->tw);
+            launch((k_rowsf<N>), dim3(g), dim3(T), 0, s, planes, items, v->tw);
         } else {
             constexpr int T = W * (N / F) / kElems;
-            const int items = ups * F * (N / W);
-            int g = persistent_grid(k_colsf<N, F, W, G>, T, items);
-            g -= g % (8 * G);  // the halves of a tile on blocks b, b + 8 at every step of the item loop
-            launch((k_colsf<N, F, W, G>), dim3(g), dim3(T), 0, s, (const float2*)scratch, planes, items, v->tw);
+            const int items = ups * (N / W);
+            int g = persistent_grid(k_colsf_ip<N, W, G>, T, items);
+            g -= g % (8 * G);  // the pieces of a tile on blocks b, b + 8, ... at every step of the item loop
+            launch((k_colsf_ip<N, W, G>), dim3(g), dim3(T), 0, s, planes, items, v->tw);
         }
         return hipGetLastError();
     }
@@ -481,9 +413,9 @@ hipError_t launch_ifft_rows_v2(const DevView& v, float2* base, int ups, hipStrea
 hipError_t launch_ifft_cols_v2(const DevView& v, float2* base, int ups, hipStream_t s) {
     return dispatch_n<Cols2>(v.n, &v, base, ups, s);
 }
-hipError_t launch_ifft_fold(const DevView& v, float2* planes, int ups, float2* scratch, int part, hipStream_t s) {
+hipError_t launch_ifft_fold(const DevView& v, float2* planes, int ups, int part, hipStream_t s) {
     if (v.n != OpFold::N) return hipErrorInvalidValue;
-    return OpFold::go(&v, planes, ups, scratch, part, s);
+    return OpFold::go(&v, planes, ups, part, s);
 }
 
 }  // namespace ocean

@@ -678,10 +678,10 @@ int ocean_ifft2d(ocean_ctx* ctx, int plane_mask) {
             for (int c0 = 0; c0 < ups; c0 += k) {
                 const int kc = std::min(k, ups - c0);
                 float2* planes = ctx->plane[p] + (size_t)c0 * up_elems;
-                if (int r = timed(ctx, 0, [&] { return ocean::launch_ifft_fold(v, planes, kc, nullptr, 0, ctx->stream); },
+                if (int r = timed(ctx, 0, [&] { return ocean::launch_ifft_fold(v, planes, kc, 0, ctx->stream); },
                                   "ifft_rows"))
                     return r;
-                if (int r = timed(ctx, 1, [&] { return ocean::launch_ifft_fold(v, planes, kc, nullptr, 1, ctx->stream); },
+                if (int r = timed(ctx, 1, [&] { return ocean::launch_ifft_fold(v, planes, kc, 1, ctx->stream); },
                                   "ifft_cols"))
                     return r;
             }

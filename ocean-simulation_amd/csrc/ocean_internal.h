@@ -114,10 +114,9 @@ hipError_t launch_ifft_rows_v2(const DevView& v, float2* base, int ups, hipStrea
 hipError_t launch_ifft_cols_v2(const DevView& v, float2* base, int ups, hipStream_t s);
 // N = 4096: the operator over `ups` consecutive unit-planes at `planes` (plane p of unit u is
 // unit-plane p * U + u) with its column transform split by decimation in frequency into two 2048-point
-// column transforms (fft2.hip k_rowsf / k_colsf); part 0 = rows + fold (planes -> scratch sub-planes),
-// 1 = the column transforms + permute (scratch -> planes) on XCD-paired 8-column tiles.  scratch ==
-// nullptr: in place (k_rowsf onto the planes, k_colsf_ip: both sub-planes of a tile per item).
-hipError_t launch_ifft_fold(const DevView& v, float2* planes, int ups, float2* scratch, int part, hipStream_t s);
+// column transforms, in place (fft2.hip): part 0 = rows + fold onto the planes' own rows (k_rowsf),
+// 1 = the column transforms + permute, both sub-planes of an XCD-paired 8-column tile per item (k_colsf_ip).
+hipError_t launch_ifft_fold(const DevView& v, float2* planes, int ups, int part, hipStream_t s);
 
 // fft3.hip: fused frame through the tile-major intermediate; the row pass
 // recomputes wave data and feeds evolve straight into a radix-4/8 first stage;
