@@ -1,8 +1,8 @@
 """CPU check of the decimation-in-frequency split the N = 4096 operator uses (fft2.hip k_rowsf /
-k_colsf): a column transform of N points as F transforms of L = N / F points over folded rows,
+k_colsf_ip, F = 2; F = 4 was an earlier form): a column transform of N points as F transforms of L = N / F points over folded rows,
     X[F m + b] = sum_{n < L} z_b[n] w_L^(n m),   z_b[n] = w_N^(n b) sum_{r < F} a[n + L r] w_F^(r b),
 with w = exp(+2 pi i / .) (the inverse transform of IFFT.compute), and the incremental radix-4 fold
-order of k_rowsf (rows r = 0, 2, 1, 3: s0, d0 = a0 +- a2, then z_0 = s0 + s1, z_2 = s0 - s1,
+order of the F = 4 row launch (rows r = 0, 2, 1, 3: s0, d0 = a0 +- a2, then z_0 = s0 + s1, z_2 = s0 - s1,
 z_1 = d0 + i d1, z_3 = d0 - i d1).  float64 numpy against N * ifft."""
 import numpy as np
 import pytest
