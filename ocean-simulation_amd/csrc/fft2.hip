@@ -124,32 +124,6 @@ __global__ __launch_bounds__(W_ * N / kElems) void k_cols2(float2* __restrict__ 
     }
 }
 
-// Per-stage tables of the L-point plan read from the context's N-point table tw[m] = exp(2 pi i m / N)
-// (the same float bits as the frame's fft4k.hip SubTw); k_colsf runs 2048-point plans in a 4096 context.
-template <int L, int N>
-struct OpSubTw {
-    using Full = StageTw<L, 16>;
-    static constexpr int S = Full::S;
-    static constexpr int kLdsEntries = Full::kEntries;
-    template <int s>
-    static __device__ __forceinline__ void load_stage(float2* lds, const float2* tw, int tid, int nthreads) {
-        if constexpr (s < S) {
-            constexpr int NS = ns_of(L, s, 16), R = radix_of(L, s, 16), O = Full::off(s);
-            for (int i = tid; i < NS * R; i += nthreads) {
-                const int r = i / NS, k = i % NS;
-                lds[O + i] = tw[(r * k * (N / (NS * R))) & (N - 1)];
-            }
-            load_stage<s + 1>(lds, tw, tid, nthreads);
-        }
-    }
-    static __device__ __forceinline__ void load(float2* lds, const float2* tw, int tid, int nthreads) {
-        load_stage<1>(lds, tw, tid, nthreads);
-    }
-    template <int ST>
-    static __device__ __forceinline__ void apply(float2* v, int j, const float2* tws) {
-        Full::template apply<ST>(v, j, tws);
-    }
-};
 
 // ------------------------------------------------- folded columns (N = 4096)
 // The column transform at N = F L (F = 2) split by decimation in frequency:
@@ -235,8 +209,7 @@ __global__ __launch_bounds__(W * (N / 2) / kElems) void k_colsf_ip(float2* plane
                                                                    const float2* __restrict__ tw) {
     constexpr int F = 2, L = N / F;
     using CT = ColTile<L, W>;  // geometry only: lanes, in_dy / out_dy
-    // W < 8: compact twiddles (6.6 instead of 18 KiB), so that two 4-column workgroups share a CU
-    using TW = std::conditional_t<(W < 8), StageTwCompactSub<L, N, 16>, OpSubTw<L, N>>;
+    using TW = SubTw<L, N>;
     using E = Engine<L, W, true, Engine<L, W, true, false>::seq_pad_ok(), 16, TW>;
     static_assert(E::THREADS == CT::T && E::R0 == CT::R0 && E::RL == CT::RL, "tile geometry");
     constexpr int T = E::THREADS;

@@ -23,33 +23,6 @@ constexpr int kL1 = 64;   // step-2 length
 constexpr int kWT = 16;   // intermediate tile width (128-byte float2 rows)
 constexpr int kSeq = 64;  // sequences per workgroup: 16 columns x 4 y1 (C1) or 4 k0 (C2)
 
-// Per-stage twiddle tables of the L-point plan, read from the context's N-point
-// table tw[m] = exp(2 pi i m / N): entry r*Ns + k = tw[r k N / (Ns R)] (same float bits).
-template <int L, int N>
-struct SubTw {
-    using Full = StageTw<L, 16>;
-    static constexpr int S = Full::S;
-    static constexpr int kEntries = Full::kEntries;
-    static constexpr int kLdsEntries = kEntries;
-    template <int s>
-    static __device__ __forceinline__ void load_stage(float2* lds, const float2* tw, int tid, int nthreads) {
-        if constexpr (s < S) {
-            constexpr int NS = ns_of(L, s, 16), R = radix_of(L, s, 16), O = Full::off(s);
-            for (int i = tid; i < NS * R; i += nthreads) {
-                const int r = i / NS, k = i % NS;
-                lds[O + i] = tw[(r * k * (N / (NS * R))) & (N - 1)];
-            }
-            load_stage<s + 1>(lds, tw, tid, nthreads);
-        }
-    }
-    static __device__ __forceinline__ void load(float2* lds, const float2* tw, int tid, int nthreads) {
-        load_stage<1>(lds, tw, tid, nthreads);
-    }
-    template <int ST>
-    static __device__ __forceinline__ void apply(float2* v, int j, const float2* tws) {
-        Full::template apply<ST>(v, j, tws);
-    }
-};
 
 // Pass C1: item = (plane, unit, 16-column tile, block of 4 y1).  Sequence
 // b = y1_local * 16 + column, element y0: intermediate slot

@@ -210,6 +210,35 @@ struct StageTwCompactSub : StageTwCompact<L, R0> {
     }
 };
 
+// Per-stage tables of an L-point plan inside a context of size N >= L, read from the context's base table
+// tw[m] = exp(2 pi i m / N): entry r*Ns + k = tw[r k N / (Ns R)] (the same float bits as StageTw<L>'s
+// double-rounded entries).  The 4096 operator's 2048-point columns and the four-step passes use it.
+template <int L, int N>
+struct SubTw {
+    using Full = StageTw<L, 16>;
+    static constexpr int S = Full::S;
+    static constexpr int kEntries = Full::kEntries;
+    static constexpr int kLdsEntries = kEntries;
+    template <int s>
+    static __device__ __forceinline__ void load_stage(float2* lds, const float2* tw, int tid, int nthreads) {
+        if constexpr (s < S) {
+            constexpr int NS = ns_of(L, s, 16), R = radix_of(L, s, 16), O = Full::off(s);
+            for (int i = tid; i < NS * R; i += nthreads) {
+                const int r = i / NS, k = i % NS;
+                lds[O + i] = tw[(r * k * (N / (NS * R))) & (N - 1)];
+            }
+            load_stage<s + 1>(lds, tw, tid, nthreads);
+        }
+    }
+    static __device__ __forceinline__ void load(float2* lds, const float2* tw, int tid, int nthreads) {
+        load_stage<1>(lds, tw, tid, nthreads);
+    }
+    template <int ST>
+    static __device__ __forceinline__ void apply(float2* v, int j, const float2* tws) {
+        Full::template apply<ST>(v, j, tws);
+    }
+};
+
 // LDS twiddle tables for plan (N, R0): the full per-stage tables when they fit, else the compact form.
 template <int N, int R0 = 16>
 using StageTwLds = std::conditional_t<StageTw<N, R0>::kInLds, StageTw<N, R0>, StageTwCompact<N, R0>>;
