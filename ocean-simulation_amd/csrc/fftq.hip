@@ -592,7 +592,16 @@ __global__ __launch_bounds__((WT ? WT : b3_w(N)) * N / kElems) void k_pass_bq(De
     };
     // item -> full tile index u * tiles + tile over the column band's tiles
     const int bt0 = v.x0 / W, bnt = v.nx / W;
-    auto full = [&](int item) { return BAND ? (item / bnt) * CT::tiles + bt0 + item % bnt : item; };
+    // Without DC (chunked frames, as cfg4's) the 32 workgroups of one XCD (blocks b, b + 8, ...) take 32
+    // consecutive tiles at each step of the item loop, so each XCD streams whole 256-column runs of the
+    // texture rows: cfg4 51.2 -> 52.0 k tile-frames/s (G = 64 the same, 128 slower); at cfg3 (DC) it does
+    // not help (docs/MEASUREMENTS.md section 8).  Needs items % (8 G) == 0, else the identity order.
+    constexpr int G = DC ? 1 : 32;
+    const bool grp = G > 1 && items % (8 * G) == 0;
+    auto full = [&](int item) {
+        if (grp) item = (item & ~(8 * G - 1)) + G * (item & 7) + ((item >> 3) & (G - 1));
+        return BAND ? (item / bnt) * CT::tiles + bt0 + item % bnt : item;
+    };
     auto win16 = [&](const float4* base, int ft) {
         const int u = ft / CT::tiles, x0 = (ft % CT::tiles) * W;
         return make_win(base + (size_t)u * N * N + x0, (unsigned)((N * N - x0) * 16));
