@@ -124,7 +124,6 @@ __global__ __launch_bounds__(W_ * N / kElems) void k_cols2(float2* __restrict__ 
     }
 }
 
-
 // ------------------------------------------------- folded columns (N = 4096)
 // The column transform at N = F L (F = 2) split by decimation in frequency:
 //   X[F m + b] = sum_{n < L} z_b[n] w_L^(n m),   z_b[n] = w_N^(n b) (a[n] + (-1)^b a[n + L]).

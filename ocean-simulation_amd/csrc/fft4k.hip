@@ -23,7 +23,6 @@ constexpr int kL1 = 64;   // step-2 length
 constexpr int kWT = 16;   // intermediate tile width (128-byte float2 rows)
 constexpr int kSeq = 64;  // sequences per workgroup: 16 columns x 4 y1 (C1) or 4 k0 (C2)
 
-
 // Pass C1: item = (plane, unit, 16-column tile, block of 4 y1).  Sequence
 // b = y1_local * 16 + column, element y0: intermediate slot
 // tile + (y1_0 * 16 + b) + y0 * (L1 * 16).  In place.
