@@ -122,6 +122,16 @@ namespace OceanHip
         }
 
         // -------------------------------------------------------- initial spectrum
+        // The initial spectrum's transcendentals, each correctly rounded (double, one rounding), as the
+        // oracle (oracle/ocean_oracle.c cr_*) and the HIP library evaluate them: h0 bit-exact across the three.
+        static float CrPow(float a, float b) => (float)Math.Pow(a, b);
+        static float CrExp(float a) => (float)Math.Exp(a);
+        static float CrLog(float a) => (float)Math.Log(a);
+        static float CrTanh(float a) => (float)Math.Tanh(a);
+        static float CrCosh(float a) => (float)Math.Cosh(a);
+        static float CrCos(float a) => (float)Math.Cos(a);
+        static float CrAtan2(float a, float b) => (float)Math.Atan2(a, b);
+
         float AngularFrequency(float k) => MathF.Sqrt(p.gravity * k);  // InitialSpectrum.compute:33-35
 
         float TMACorrection(float w)  // :38-43
@@ -134,54 +144,54 @@ namespace OceanHip
 
         float JONSWAP(float w, float wp)  // :47-56
         {
-            float alpha = 0.076f * MathF.Pow(MathF.Abs(p.windSpeed * p.windSpeed / (p.fetch * p.gravity)), 0.22f);
+            float alpha = 0.076f * CrPow(MathF.Abs(p.windSpeed * p.windSpeed / (p.fetch * p.gravity)), 0.22f);
             float gamma = 3.3f;
             float sigma = w <= wp ? 0.07f : 0.09f;
             float d = w - wp;
-            float r = MathF.Exp(-(d * d) / (2.0f * sigma * sigma * wp * wp));
-            return alpha * p.gravity * p.gravity / MathF.Pow(w, 5.0f) * MathF.Exp(-1.25f * MathF.Pow(wp / w, 4.0f)) *
-                   MathF.Pow(MathF.Abs(gamma), r);
+            float r = CrExp(-(d * d) / (2.0f * sigma * sigma * wp * wp));
+            return alpha * p.gravity * p.gravity / CrPow(w, 5.0f) * CrExp(-1.25f * CrPow(wp / w, 4.0f)) *
+                   CrPow(MathF.Abs(gamma), r);
         }
 
         float SpreadPower(float w, float wp)  // :60-66
         {
-            if (w < 1.05f * wp) return 6.97f * MathF.Pow(MathF.Abs(w / wp), 4.06f);
+            if (w < 1.05f * wp) return 6.97f * CrPow(MathF.Abs(w / wp), 4.06f);
             float peakSpeed = p.gravity / wp;
             float mu = -2.33f - 1.45f * (p.windSpeed / peakSpeed - 1.17f);
-            return 9.77f * MathF.Pow(MathF.Abs(w / wp), mu);
+            return 9.77f * CrPow(MathF.Abs(w / wp), mu);
         }
 
         static float NormalizationFactor(float s)  // :69-74
         {
             float s2 = s * s, s3 = s2 * s;
             if (s <= 0.4f)
-                return 0.09f * s3 + (MathF.Pow(MathF.Log(2.0f), 2.0f) / PI - PI / 12.0f) * s2 + MathF.Log(2.0f) / PI * s +
+                return 0.09f * s3 + (CrPow(CrLog(2.0f), 2.0f) / PI - PI / 12.0f) * s2 + CrLog(2.0f) / PI * s +
                        1.0f / (2.0f * PI);
             return MathF.Sqrt(s) / (2.0f * MathF.Sqrt(PI)) + 1.0f / (16.0f * MathF.Sqrt(PI * s));
         }
 
         float DirectionalSpread(float w, float wp, float theta, float swell)  // :78-84
         {
-            float s = SpreadPower(w, wp) + 16.0f * MathF.Tanh(w / wp) * swell * swell;
+            float s = SpreadPower(w, wp) + 16.0f * CrTanh(w / wp) * swell * swell;
             float len = MathF.Sqrt(p.windDirX * p.windDirX + p.windDirY * p.windDirY);  // normalize(_WindDirection)
-            float windTheta = MathF.Atan2(p.windDirY / len, p.windDirX / len);
-            return NormalizationFactor(s) * MathF.Pow(MathF.Abs(MathF.Cos(0.5f * (theta - windTheta))), 2.0f * s);
+            float windTheta = CrAtan2(p.windDirY / len, p.windDirX / len);
+            return NormalizationFactor(s) * CrPow(MathF.Abs(CrCos(0.5f * (theta - windTheta))), 2.0f * s);
         }
 
         float FrequencyDerivative(float k, float w)  // :87-91
         {
-            float th = MathF.Tanh(MathF.Min(k * p.depth, 20.0f));
-            float ch = MathF.Cosh(k * p.depth);
+            float th = CrTanh(MathF.Min(k * p.depth, 20.0f));
+            float ch = CrCosh(k * p.depth);
             return p.gravity * (p.depth * k / ch / ch + th) / (w * 2.0f);
         }
 
-        static float ShortWavesFade(float k, float fade) => MathF.Exp(-fade * fade * k * k);  // :95-97
+        static float ShortWavesFade(float k, float fade) => CrExp(-fade * fade * k * k);  // :95-97
 
         // CalculateInitialSpectrumTextures (WaterBody.cs:171-178): :99-129 then :135-143.
         public void CalculateInitialSpectrumTextures()
         {
             int n = N, half = n / 2;
-            float wp = 22.0f * MathF.Pow(MathF.Abs(p.gravity * p.gravity / (p.windSpeed * p.fetch)), 0.3333f);  // :118
+            float wp = 22.0f * CrPow(MathF.Abs(p.gravity * p.gravity / (p.windSpeed * p.fetch)), 0.3333f);  // :118
             for (int c = 0; c < C; c++)
             {
                 float dk = 2.0f * PI / cascades[c].wavelength;  // :110
@@ -194,7 +204,7 @@ namespace OceanHip
                         float kmag = MathF.Sqrt(kx * kx + kz * kz);
                         if (kmag >= cascades[c].cutoffLow && kmag <= cascades[c].cutoffHigh)
                         {
-                            float kangle = MathF.Atan2(kz, kx);
+                            float kangle = CrAtan2(kz, kx);
                             float w = AngularFrequency(kmag);
                             float amp = MathF.Sqrt(2.0f * TMACorrection(w) * JONSWAP(w, wp) *
                                                    DirectionalSpread(w, wp, kangle, cascades[c].swell) *

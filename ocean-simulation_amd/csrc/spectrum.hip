@@ -19,6 +19,19 @@ struct Sp {
 
 // AngularFrequency (:33-35) = sqrt(g |k|) lives in wave_data (spectrum_math.h).
 
+// The transcendentals of the initial spectrum, each correctly rounded: evaluated in double and rounded
+// once to fp32, as the oracle does (oracle/ocean_oracle.c cr_*), so h0 is bit-exact between the two.
+// The device's fp32 powf / expf / atan2f / ... differed from it in 63-72 % of h0 texels by a few ulp,
+// and that difference was the whole of the library's pointwise excess over the oracle's own fp32 error
+// (2.5-3.0x, tools/pointwise_stages.py, docs/MEASUREMENTS.md section 9).  Runs once per init.
+__device__ __forceinline__ float sp_pow(float a, float b) { return (float)pow((double)a, (double)b); }
+__device__ __forceinline__ float sp_exp(float a) { return (float)exp((double)a); }
+__device__ __forceinline__ float sp_log(float a) { return (float)log((double)a); }
+__device__ __forceinline__ float sp_tanh(float a) { return (float)tanh((double)a); }
+__device__ __forceinline__ float sp_cosh(float a) { return (float)cosh((double)a); }
+__device__ __forceinline__ float sp_cos(float a) { return (float)cos((double)a); }
+__device__ __forceinline__ float sp_atan2(float a, float b) { return (float)atan2((double)a, (double)b); }
+
 __device__ __forceinline__ float tma_correction(const Sp& p, float w) {  // :38-43
     float wh = w * sqrtf(p.D / p.g);
     if (wh <= 1.0f) return 0.5f * wh * wh;
@@ -27,51 +40,51 @@ __device__ __forceinline__ float tma_correction(const Sp& p, float w) {  // :38-
 }
 
 __device__ __forceinline__ float jonswap(const Sp& p, float w, float wp) {  // :47-56
-    float alpha = 0.076f * powf(fabsf(p.U * p.U / (p.F * p.g)), 0.22f);
+    float alpha = 0.076f * sp_pow(fabsf(p.U * p.U / (p.F * p.g)), 0.22f);
     float gamma = 3.3f;
     float sigma = w <= wp ? 0.07f : 0.09f;
     float d = w - wp;
-    float r = expf(-(d * d) / (2.0f * sigma * sigma * wp * wp));
-    return alpha * p.g * p.g / powf(w, 5.0f) * expf(-1.25f * powf(wp / w, 4.0f)) * powf(fabsf(gamma), r);
+    float r = sp_exp(-(d * d) / (2.0f * sigma * sigma * wp * wp));
+    return alpha * p.g * p.g / sp_pow(w, 5.0f) * sp_exp(-1.25f * sp_pow(wp / w, 4.0f)) * sp_pow(fabsf(gamma), r);
 }
 
 __device__ __forceinline__ float spread_power(const Sp& p, float w, float wp) {  // :60-66
-    if (w < 1.05f * wp) return 6.97f * powf(fabsf(w / wp), 4.06f);
+    if (w < 1.05f * wp) return 6.97f * sp_pow(fabsf(w / wp), 4.06f);
     float peak_speed = p.g / wp;
     float mu = -2.33f - 1.45f * (p.U / peak_speed - 1.17f);
-    return 9.77f * powf(fabsf(w / wp), mu);
+    return 9.77f * sp_pow(fabsf(w / wp), mu);
 }
 
 __device__ __forceinline__ float normalization_factor(float s) {  // :69-74
     float s2 = s * s;
     float s3 = s2 * s;
     if (s <= 0.4f)
-        return 0.09f * s3 + (powf(logf(2.0f), 2.0f) / kPi - kPi / 12.0f) * s2 + logf(2.0f) / kPi * s +
+        return 0.09f * s3 + (sp_pow(sp_log(2.0f), 2.0f) / kPi - kPi / 12.0f) * s2 + sp_log(2.0f) / kPi * s +
                1.0f / (2.0f * kPi);
     return sqrtf(s) / (2.0f * sqrtf(kPi)) + 1.0f / (16.0f * sqrtf(kPi * s));
 }
 
 __device__ __forceinline__ float directional_spread(const Sp& p, float w, float wp, float theta, float swell) {  // :78-84
-    float s = spread_power(p, w, wp) + 16.0f * tanhf(w / wp) * swell * swell;
+    float s = spread_power(p, w, wp) + 16.0f * sp_tanh(w / wp) * swell * swell;
     float len = sqrtf(p.wdx * p.wdx + p.wdy * p.wdy);  // normalize(float2(x, y))
-    float wind_theta = atan2f(p.wdy / len, p.wdx / len);
-    return normalization_factor(s) * powf(fabsf(cosf(0.5f * (theta - wind_theta))), 2.0f * s);
+    float wind_theta = sp_atan2(p.wdy / len, p.wdx / len);
+    return normalization_factor(s) * sp_pow(fabsf(sp_cos(0.5f * (theta - wind_theta))), 2.0f * s);
 }
 
 __device__ __forceinline__ float frequency_derivative(const Sp& p, float k, float w) {  // :87-91
-    float th = tanhf(fminf(k * p.D, 20.0f));
-    float ch = coshf(k * p.D);
+    float th = sp_tanh(fminf(k * p.D, 20.0f));
+    float ch = sp_cosh(k * p.D);
     return p.g * (p.D * k / ch / ch + th) / (w * 2.0f);
 }
 
-__device__ __forceinline__ float short_waves_fade(float k, float fade) { return expf(-fade * fade * k * k); }  // :95-97
+__device__ __forceinline__ float short_waves_fade(float k, float fade) { return sp_exp(-fade * fade * k * k); }  // :95-97
 
 // CalculateInitialSpectrumTextures (:99-129): one thread per (unit, texel).
 __global__ __launch_bounds__(256) void k_init_spectrum(DevView v, Sp p) {
     const int n = v.n;
     const size_t plane = (size_t)n * n;
     const size_t total = plane * v.units;
-    const float wp = 22.0f * powf(fabsf(p.g * p.g / (p.U * p.F)), 0.3333f);  // :118
+    const float wp = 22.0f * sp_pow(fabsf(p.g * p.g / (p.U * p.F)), 0.3333f);  // :118
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
         const int u = (int)(i / plane);
         const size_t t = i - (size_t)u * plane;
@@ -84,7 +97,7 @@ __global__ __launch_bounds__(256) void k_init_spectrum(DevView v, Sp p) {
         const float4 w = wave_data(x, y, n, wave_band(cs), p.g, &kmag);
         float4 h;
         if (kmag >= cs[1] && kmag <= cs[2]) {  // :114
-            const float kangle = atan2f(w.z, w.x);
+            const float kangle = sp_atan2(w.z, w.x);
             const float om = w.w;  // angular_frequency(kmag) (:116), computed in wave_data
             const float amp = sqrtf(2.0f * tma_correction(p, om) * jonswap(p, om, wp) *
                                     directional_spread(p, om, wp, kangle, cs[3]) * short_waves_fade(kmag, cs[4]) *

@@ -21,9 +21,17 @@
  *   frame schedule  WaterBody.cs:180-193
  *
  * All arithmetic is IEEE fp32 in the reference's operation order (compile with
- * -ffp-contract=off so no FMA contraction changes roundings).  Transcendentals
- * come from glibc's libm (the reference uses the GPU vendor's HLSL intrinsics;
- * that difference is covered by the stated tolerance).
+ * -ffp-contract=off so no FMA contraction changes roundings).  The initial
+ * spectrum's transcendentals (pow, exp, log, tanh, cosh, cos, atan2 of
+ * InitialSpectrum.compute:33-129) are each its correctly rounded fp32 value:
+ * evaluated in double and rounded once (cr_* below).  The reference's HLSL
+ * intrinsics have vendor-defined precision, so no libm reproduces them; the
+ * correctly rounded value is the one implementation-independent fp32 statement
+ * of each call, and the HIP library evaluates the same way, so h0 is bit-exact
+ * between the two.  glibc 2.35's fp32 functions instead differ from it in
+ * 7-10 % of h0 texels (atan2f 6.4 %, cosf 0.9 %, tanhf 0.16 %, powf 0.06 %,
+ * expf 0.05 % at 4 x 1024^2; docs/MEASUREMENTS.md section 9).  The per-frame
+ * phase uses glibc's sinf / cosf, the noise glibc's logf.
  *
  * Parity status: the reference ships no tests, fixtures or golden vectors and
  * cannot be built or run here (Unity + HLSL, no C# toolchain).
@@ -114,6 +122,15 @@ void oracle_generate_noise(int n, uint64_t seed, float *noise) {
 /* ------------------------------------------------------------------------ */
 /* Initial spectrum: InitialSpectrum.compute:33-129                          */
 /* ------------------------------------------------------------------------ */
+/* Correctly rounded fp32 transcendentals (see the header). */
+static float cr_pow(float a, float b) { return (float)pow((double)a, (double)b); }
+static float cr_exp(float a) { return (float)exp((double)a); }
+static float cr_log(float a) { return (float)log((double)a); }
+static float cr_tanh(float a) { return (float)tanh((double)a); }
+static float cr_cosh(float a) { return (float)cosh((double)a); }
+static float cr_cos(float a) { return (float)cos((double)a); }
+static float cr_atan2(float a, float b) { return (float)atan2((double)a, (double)b); }
+
 static float or_angular_frequency(const or_params *p, float k) { /* :33-35 */
     return sqrtf(p->gravity * k);
 }
@@ -126,48 +143,48 @@ static float or_tma(const or_params *p, float w) { /* :38-43 */
 }
 
 static float or_jonswap(const or_params *p, float w, float wp) { /* :47-56 */
-    float alpha = 0.076f * powf(fabsf(p->wind_speed * p->wind_speed / (p->fetch * p->gravity)), 0.22f);
+    float alpha = 0.076f * cr_pow(fabsf(p->wind_speed * p->wind_speed / (p->fetch * p->gravity)), 0.22f);
     float gamma = 3.3f;
     float sigma = w <= wp ? 0.07f : 0.09f;
     float d = w - wp;
-    float r = expf(-(d * d) / (2.0f * sigma * sigma * wp * wp));
-    return alpha * p->gravity * p->gravity / powf(w, 5.0f) * expf(-1.25f * powf(wp / w, 4.0f)) *
-           powf(fabsf(gamma), r);
+    float r = cr_exp(-(d * d) / (2.0f * sigma * sigma * wp * wp));
+    return alpha * p->gravity * p->gravity / cr_pow(w, 5.0f) * cr_exp(-1.25f * cr_pow(wp / w, 4.0f)) *
+           cr_pow(fabsf(gamma), r);
 }
 
 static float or_spread_power(const or_params *p, float w, float wp) { /* :60-66 */
-    if (w < 1.05f * wp) return 6.97f * powf(fabsf(w / wp), 4.06f);
+    if (w < 1.05f * wp) return 6.97f * cr_pow(fabsf(w / wp), 4.06f);
     float peak_speed = p->gravity / wp;
     float mu = -2.33f - 1.45f * (p->wind_speed / peak_speed - 1.17f);
-    return 9.77f * powf(fabsf(w / wp), mu);
+    return 9.77f * cr_pow(fabsf(w / wp), mu);
 }
 
 static float or_normalization(float s) { /* :69-74 */
     float s2 = s * s;
     float s3 = s2 * s;
     if (s <= 0.4f)
-        return 0.09f * s3 + (powf(logf(2.0f), 2.0f) / OR_PI - OR_PI / 12.0f) * s2 + logf(2.0f) / OR_PI * s +
+        return 0.09f * s3 + (cr_pow(cr_log(2.0f), 2.0f) / OR_PI - OR_PI / 12.0f) * s2 + cr_log(2.0f) / OR_PI * s +
                1.0f / (2.0f * OR_PI);
     return sqrtf(s) / (2.0f * sqrtf(OR_PI)) + 1.0f / (16.0f * sqrtf(OR_PI * s));
 }
 
 static float or_directional_spread(const or_params *p, float w, float wp, float theta, float swell) { /* :78-84 */
-    float s = or_spread_power(p, w, wp) + 16.0f * tanhf(w / wp) * swell * swell;
+    float s = or_spread_power(p, w, wp) + 16.0f * cr_tanh(w / wp) * swell * swell;
     /* normalize(float2(x, y)): v / |v| */
     float len = sqrtf(p->wind_dir_x * p->wind_dir_x + p->wind_dir_y * p->wind_dir_y);
     float nx = p->wind_dir_x / len, ny = p->wind_dir_y / len;
-    float wind_theta = atan2f(ny, nx);
-    return or_normalization(s) * powf(fabsf(cosf(0.5f * (theta - wind_theta))), 2.0f * s);
+    float wind_theta = cr_atan2(ny, nx);
+    return or_normalization(s) * cr_pow(fabsf(cr_cos(0.5f * (theta - wind_theta))), 2.0f * s);
 }
 
 static float or_frequency_derivative(const or_params *p, float k, float w) { /* :87-91 */
-    float th = tanhf(fminf(k * p->depth, 20.0f));
-    float ch = coshf(k * p->depth);
+    float th = cr_tanh(fminf(k * p->depth, 20.0f));
+    float ch = cr_cosh(k * p->depth);
     return p->gravity * (p->depth * k / ch / ch + th) / (w * 2.0f);
 }
 
 static float or_short_waves_fade(float k, float fade) { /* :95-97 */
-    return expf(-fade * fade * k * k);
+    return cr_exp(-fade * fade * k * k);
 }
 
 /* CalculateInitialSpectrumTextures (:99-129) for all C cascades.
@@ -175,7 +192,7 @@ static float or_short_waves_fade(float k, float fade) { /* :95-97 */
 void oracle_init_spectrum(int n, int ncasc, const or_params *p, const or_cascade *cs, const float *noise, float *h0,
                           float *waves) {
     int half = n / 2;
-    float wp = 22.0f * powf(fabsf(p->gravity * p->gravity / (p->wind_speed * p->fetch)), 0.3333f); /* :118 */
+    float wp = 22.0f * cr_pow(fabsf(p->gravity * p->gravity / (p->wind_speed * p->fetch)), 0.3333f); /* :118 */
     for (int c = 0; c < ncasc; c++) {
         float dk = 2.0f * OR_PI / cs[c].wavelength; /* :110 */
         for (int y = 0; y < n; y++)
@@ -187,7 +204,7 @@ void oracle_init_spectrum(int n, int ncasc, const or_params *p, const or_cascade
                 float kx = (float)nx * dk, kz = (float)nz * dk;
                 float kmag = sqrtf(kx * kx + kz * kz);
                 if (kmag >= cs[c].cutoff_low && kmag <= cs[c].cutoff_high) {
-                    float kangle = atan2f(kz, kx);
+                    float kangle = cr_atan2(kz, kx);
                     float w = or_angular_frequency(p, kmag);
                     float amp = sqrtf(2.0f * or_tma(p, w) * or_jonswap(p, w, wp) *
                                       or_directional_spread(p, w, wp, kangle, cs[c].swell) *

@@ -61,7 +61,9 @@ def test_init_spectrum(n, shallow):
     g_h0, g_w = ctx.read_all(oh.TEX_H0), ctx.read_all(oh.TEX_WAVES)
     # kx, kz, 1/|k| and omega use only correctly rounded + - * / sqrt: bit-exact
     np.testing.assert_array_equal(g_w, waves)
-    assert_channels(g_h0, h0, what="h0")
+    # h0: every transcendental correctly rounded on both sides (spectrum.hip sp_*, ocean_oracle.c cr_*), the
+    # fp32 arithmetic between them in the same order: bit-exact too, conjugate partner .zw included
+    np.testing.assert_array_equal(g_h0, h0)
     ctx.close()
 
 
@@ -223,6 +225,7 @@ def test_golden_fixtures(flags):
         ctx.generate_noise(case["seed"])
         np.testing.assert_array_equal(ctx.read(oh.TEX_NOISE), z["noise"])
         ctx.init_spectrum()
+        np.testing.assert_array_equal(ctx.read_all(oh.TEX_H0), z["h0"])  # correctly rounded init: bit-exact
         for f, t in enumerate(case["times"]):
             ctx.step(t)
             assert_channels(ctx.read_all(oh.TEX_DISP)[..., :3], z[f"disp_{f}"][..., :3], what=f"{case['name']} disp {f}")
@@ -270,14 +273,20 @@ def test_frames_vs_oracle(n, ncasc, flags):
 
 
 # SURVEY.md section 7's second tolerance clause (pointwise 1e-5 where |b| >= 1e-3 max|b|) is infeasible for
-# the reference's own algorithm in fp32: on that mask the radix-2 fp32 oracle is 2.4e-4 .. 1.0e-2 away from
-# the float64 frame (tools/pointwise.py, profiles/r05_pointwise/pointwise.json).  The
-# replacement asserted here, per frame, cascade and output channel on the same mask: the library's pointwise
-# error against float64 is within PW_FACTOR of the oracle's own, and so is its pointwise distance to the
-# oracle.  Measured worst ratios: 2.5 / 2.9 (cfg2), 3.0 / 3.3 (cfg3), 2.2 / 2.1 (cfg5), the height channel
-# Dy in each (it shares its complex transform with Dyx, which is larger at short wavelengths).
+# the reference's own algorithm in fp32: on that mask the radix-2 fp32 oracle is 7e-4 .. 1.0e-2 away from
+# the float64 frame (tools/pointwise.py, profiles/r06_pointwise/pointwise.json).  This is a
+# stated deviation from the spec.  What is asserted instead, per frame, cascade and output channel on the same
+# mask, with `own` = the oracle's pointwise error against float64:
+#   mine <= PW_CEILING[n][0] * own   the library's pointwise error against float64
+#   dist <= PW_CEILING[n][1] * own   its pointwise distance to the oracle
+# Since round 6 h0 is bit-exact between the two (correctly rounded init on both sides), so these measure
+# the per-frame arithmetic alone.  The ceilings are the measured worst over channels, cascades and frames
+# (profiles/r06_pointwise: mine 1.006 / 1.116 / 0.835, dist 1.547 / 1.601 / 1.258 at cfg2 / cfg3 / cfg5)
+# plus about 10 %.  dist near sqrt(2) is what two fp32 computations with independent rounding errors of the
+# oracle's size give.  (Round 5's single factor 4 covered the init's device-libm h0, then 63-72 % of texels
+# a few ulp off: the whole of the 2.5-3.0x excess, tools/pointwise_stages.py.)
 PW_FRAC = 1e-3
-PW_FACTOR = 4.0
+PW_CEILING = {512: (1.10, 1.70), 1024: (1.25, 1.80), 4096: (1.00, 1.40)}
 
 
 def _f64_frame(h0, waves, t, foam_prev, full):
@@ -326,8 +335,9 @@ def test_pointwise_clause(n, ncasc, flags, times):
                         own, _ = O.pointwise_err(b, x, PW_FRAC)
                         mine, _ = O.pointwise_err(a, x, PW_FRAC)
                         dist, _ = O.pointwise_err(a, b, PW_FRAC)
-                        assert mine <= PW_FACTOR * own, f"{what}: pointwise vs float64 {mine:.2e} > {PW_FACTOR} x {own:.2e}"
-                        assert dist <= PW_FACTOR * own, f"{what}: pointwise vs oracle {dist:.2e} > {PW_FACTOR} x {own:.2e}"
+                        fm, fd = PW_CEILING[n]
+                        assert mine <= fm * own, f"{what}: pointwise vs float64 {mine:.2e} > {fm} x {own:.2e}"
+                        assert dist <= fd * own, f"{what}: pointwise vs oracle {dist:.2e} > {fd} x {own:.2e}"
     finally:
         O.set_threads(1)
         ctx.close()
