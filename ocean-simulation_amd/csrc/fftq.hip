@@ -110,19 +110,9 @@ __device__ __forceinline__ float2* q_side(const DevView& v, int u) { return v.qs
 // that the chunk's three planes lie within 4 GiB of the base (go_aq), else the 64-bit form runs.
 // Three workgroups per CU (43.5 KiB of LDS each at N = 1024) need <= 168 VGPRs: the split pass 1 below
 // takes 170 unconstrained, 168 with two spilled.
-// REV (OCEAN_AQ_REV): row y2 is held as its reversed sequence w[x] = z2[(N - x) % N].  Lane j's mirror texels
-// N - x_r are then w at x_r, i.e. stage-0 butterfly j of w, so row y2 goes to LDS with the same put as row
-// y1 (no unmirror).  The mirrored put (butterfly jm = N/4 - j) costs 8 conflict cycles per ds_write2_b64
-// under the write banking of 16-lane groups mod 32 dwords (tools/ldsbench.hip: 192 cycles per item, all of
-// pass AQ's SQ_LDS_BANK_CONFLICT), and no one-per-16 padding can make both orders conflict-free.  The
-// transform of w is Z2[(N - k) % N], so output k of a y2 slot is stored to column (N - k) % N.
-#ifndef OCEAN_AQ_REV
-#define OCEAN_AQ_REV 0
-#endif
 template <int N, bool BAND = false, int WT = 0, bool OFF32 = true>
 __global__ __launch_bounds__(N / 4) __attribute__((amdgpu_waves_per_eu(N == 1024 ? 3 : 1, N == 1024 ? 3 : 10))) void
 k_pass_aq(DevView v, float time, int items) {
-    constexpr bool REV = OCEAN_AQ_REV;
     constexpr int R0 = 4, NJ = N / R0;
     constexpr int IPU = N / 2 + 1;  // items per unit
     using TW = StageTw<N, R0>;
@@ -210,17 +200,10 @@ k_pass_aq(DevView v, float time, int items) {
                     mir[p][r] = qb.q[p];
                 }
             }
-            if constexpr (REV) {  // row y2 reversed: lane j holds butterfly j of w as it is
-#pragma unroll
-                for (int p = 0; p < 3; ++p)
-#pragma unroll
-                    for (int r = 0; r < R0; ++r) g[2 * p + 1][r] = mir[p][r];
-            } else {
-                unmirror(mir[0], g[1]);
-                unmirror(mir[1], g[3]);
-                unmirror(mir[2], g[5]);
-            }
-            if (!REV && y1 == 0) {  // srow's input stays in natural order (butterfly j)
+            unmirror(mir[0], g[1]);
+            unmirror(mir[1], g[3]);
+            unmirror(mir[2], g[5]);
+            if (y1 == 0) {  // srow's input stays in natural order (butterfly j)
 #pragma unroll
                 for (int r = 0; r < R0; ++r) g[5][r] = mir[2][r];
             }
@@ -239,10 +222,10 @@ k_pass_aq(DevView v, float time, int items) {
             if (ps == 0) {
                 if (SPLIT) __syncthreads();  // the previous item's pass 1 (waves 2, 3) has read slots 2, 3
 #pragma unroll
-                for (int k = 0; k < 4; ++k) put(k, (!REV && (k & 1)) ? jm : j, g[k]);
+                for (int k = 0; k < 4; ++k) put(k, (k & 1) ? jm : j, g[k]);
             } else {
                 put(Q3SLOT, j, g[4]);
-                put(Q3SLOT + 1, (!REV && y1) ? jm : j, g[5]);
+                put(Q3SLOT + 1, y1 ? jm : j, g[5]);
             }
             __syncthreads();
             auto emit = [&](int m, int q, float2 val) {
@@ -254,28 +237,6 @@ k_pass_aq(DevView v, float time, int items) {
                 const int x = jj + q * NSL;
                 if (s && self) {  // self-mirror row: a duplicate, or row 0's srow
                     if (p == 2 && y1 == 0) q_side(v, u)[N + x] = val;
-                    return;
-                }
-                // REV, row y2: output x is column (N - x) % N (see REV above)
-                const bool rev = REV && s;
-                if (BAND && (unsigned)((rev ? (N - x) & (N - 1) : x) - v.x0) >= (unsigned)v.nx) return;  // outside the band
-                if constexpr (REV && !OFF32) {
-                    const int xc = rev ? (N - x) & (N - 1) : x;
-                    v.tplane[(size_t)p * v.inter_stride + ((size_t)u * TILES * N + (s ? y2 : y1)) * W +
-                             (size_t)(xc / W) * N * W + (xc % W)] = val;
-                    return;
-                }
-                if constexpr (REV && OFF32) {
-                    // x = jj + q NSL with NSL a multiple of W: column x is the lane's column plus q NSL / W tiles;
-                    // reversed, column (N - jj) - q NSL is the lane's reversed column minus q NSL / W tiles, except
-                    // output 0 (q = 0, jj = 0), which is column 0
-                    constexpr unsigned QS = (unsigned)((NSL / W) * N * W * 8);
-                    const unsigned lf = (unsigned)(((jj / W) * N * W + (jj % W)) * 8);
-                    const unsigned lr = (unsigned)((((N / W) - (jj + W - 1) / W) * N * W + ((W - jj % W) % W)) * 8);
-                    unsigned lo = rev ? lr - (unsigned)q * QS : lf + (unsigned)q * QS;
-                    if (rev && q == 0 && jj == 0) lo = 0u;
-                    const unsigned off = (unsigned)p * (unsigned)(v.inter_stride * 8) + (unsigned)((s ? y2 : y1) * W * 8) + lo;
-                    *(float2*)(wunit.p + (store_off_t)off) = val;
                     return;
                 }
                 if (BAND && (unsigned)(x - v.x0) >= (unsigned)v.nx) return;  // outside the column band
