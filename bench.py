@@ -374,100 +374,115 @@ def numa_placement(device, host_ptrs):
     return out
 
 
+def _loop_mode(wb, steps, warmup, f0):
+    """One readback mode of update_loop: warm-up by time, `steps` timed Update frames with no timing
+    events anywhere (frames/s), then the same loop with readback timing on (the copies' own time,
+    ocean_readback_copy_ms) and again with the frame's kernels timed (are the frames stretched by the
+    copies beside them?).  Returns (record, next frame index)."""
+    ctx = wb.ctx
+    f = f0
+    w0 = time.perf_counter()
+    while f - f0 < max(warmup, 2 * len(wb._ring)) or time.perf_counter() - w0 < UPDATE_WARM_S:
+        wb.Update(f / 60.0)
+        f += 1
+    wb.WaitForReadback()
+    warm_frames, warm_s = f - f0, time.perf_counter() - w0
+    t0 = time.perf_counter()
+    for k in range(steps):
+        wb.Update((f + k) / 60.0)
+    wb.WaitForReadback()  # every requested readback has landed inside the timed region
+    loop_s = (time.perf_counter() - t0) / steps
+    f += steps
+    wb.readback_copy_ms = []
+    for k in range(steps):
+        wb.Update((f + k) / 60.0)
+    wb.WaitForReadback()
+    f += steps
+    copies = list(wb.readback_copy_ms)
+    wb.readback_copy_ms = None
+    ctx.set_kernel_timing(True)
+    ctx.kernel_stats(0), ctx.kernel_stats(1), ctx.kernel_stats(2)
+    for k in range(steps):
+        wb.Update((f + k) / 60.0)
+    wb.WaitForReadback()
+    f += steps
+    la, _ = ctx.kernel_stats(0)
+    lb, _ = ctx.kernel_stats(1)
+    lm, _ = ctx.kernel_stats(2)
+    ctx.set_kernel_timing(False)
+    slice_bytes = wb.texturesSize ** 2 * (4 if wb.readback == "height" else 16)
+    copy_ms = float(np.median(copies)) if copies else None
+    rec = {"readback": wb.readback, "frames_per_s": round(1.0 / loop_s, 2), "ms_per_frame": round(1e3 * loop_s, 4),
+           "timed_frames": steps, "warmup": {"frames": warm_frames, "seconds": round(warm_s, 3)},
+           "pcie_bytes_per_frame": slice_bytes, "pcie_GBs": round(slice_bytes / loop_s / 1e9, 2),
+           "d2h": {"copies": len(copies), "median_ms": round(copy_ms, 4) if copy_ms else None,
+                   "max_ms": round(max(copies), 4) if copies else None,
+                   "GBs": round(slice_bytes / (copy_ms * 1e-3) / 1e9, 2) if copy_ms else None,
+                   "how": "ocean_readback_copy_ms (readback timing on, a loop of its own): HIP events on the copy "
+                          "stream around each device-to-host copy"},
+           "kernel_us_in_loop": {"pass_a": round(1e3 * la / steps, 2), "pass_b": round(1e3 * lb / steps, 2),
+                                 "other": round(1e3 * lm / steps, 2)}}
+    return rec, f
+
+
 def update_loop(steps=200, warmup=20):
     """The reference's per-frame loop at cfg3, as a Unity host over this library runs it
     (WaterBody.Update, WaterBody.cs:284-297): CalculateWavesTexturesAtTime with the mip chains of DERIV
     and TURB regenerated every frame (GenerateMips, :191-192; OCEAN_F_MIPS), then one asynchronous
     readback of displacement slice 0 per frame (AsyncGPUReadback.Request, :288) into the facade's
-    pinned ring, polled, the landed slice kept in its pinned slot for GetWaterHeight (the reference
-    copies it out, request.GetData<Color>().ToArray(), :295; the facade's buoyancyData copies on
-    access) -- ocean_hip.WaterBody.Update.  Reported beside `value` (the device frame without mips):
-    frames/s of that loop, its PCIe bytes per frame, the frame with mips alone, and the mip kernels' time
-    per frame from HIP events.
+    pinned ring, polled, the landed slice kept in its pinned slot for GetWaterHeight -- ocean_hip.WaterBody.Update.
+    Two readback modes, each its own facade and loop: "height" (the facade's default: DISP.y alone,
+    ocean_read_height_async, 4 MiB per frame -- the reference's buoyancyData is private, WaterBody.cs:58,
+    and GetWaterHeight reads only .g, :208) and "rgba" (the whole 16 MiB Color slice, as the reference
+    requests it).  Reported beside `value` (the device frame without mips): each mode's
+    frames/s with no timing events in its timed region, its PCIe bytes, the copies' own time (a second
+    loop with readback timing on) and the frame's kernels inside the loop (a third, HIP events); the
+    frame with mips alone, and the mip kernels' time.
     Warm-up is by time, not by count: the loop's first frames in a process run 3-13x slower
-    (tools/update_ramp.py, docs/MEASUREMENTS.md section 8), so a count sized for --steps 500 left the
-    driver's --steps 20 --warmup 5 timing the ramp (1.09 k against 3.02 k frames/s).  Both the frame
-    and the loop run for >= UPDATE_WARM_S (and >= `warmup` frames) before their timed regions.
-    Attribution: `d2h` = the device-to-host copies' own duration (ocean_readback_copy_ms: events on the
-    copy stream around each copy) -> the link's GB/s; `kernel_us_in_loop` = the frame's kernels timed
-    inside the loop (HIP events), against `step_with_mips.kernel_us`; `numa` = where the GPU, the
-    calling CPU and the pinned ring sit."""
-    wb = oh.scene_water_body(n=1024, n_cascades=4, seed=20251121).Awake()
-    ctx = wb.ctx
-    try:
-        f = 0
-        w0 = time.perf_counter()
-        while f < warmup or time.perf_counter() - w0 < UPDATE_WARM_S:
-            ctx.step(f / 60.0)
-            f += 1
-            if f % 16 == 0:
+    (tools/update_ramp.py, docs/MEASUREMENTS.md section 8).  Every loop runs for >= UPDATE_WARM_S (and
+    >= `warmup` frames) before its timed region."""
+    out = {"workload": "cfg3 (4 x 1024^2) frame + GenerateMips of DERIV and TURB + AsyncGPUReadback of DISP "
+                       "slice 0 every frame, ocean_hip.WaterBody.Update (WaterBody.cs:284-297)"}
+    for mode in ("height", "rgba"):
+        wb = oh.scene_water_body(n=1024, n_cascades=4, seed=20251121, readback=mode).Awake()
+        ctx = wb.ctx
+        try:
+            if mode == "height":  # the frame with mips alone, once
+                f = 0
+                w0 = time.perf_counter()
+                while f < warmup or time.perf_counter() - w0 < UPDATE_WARM_S:
+                    ctx.step(f / 60.0)
+                    f += 1
+                    if f % 16 == 0:
+                        ctx.synchronize()
                 ctx.synchronize()
-        ctx.synchronize()
-        t0 = time.perf_counter()
-        for k in range(steps):
-            ctx.step((f + k) / 60.0)
-        ctx.synchronize()
-        step_s = (time.perf_counter() - t0) / steps
-        ctx.set_kernel_timing(True)
-        ctx.kernel_stats(0), ctx.kernel_stats(1), ctx.kernel_stats(2)
-        for k in range(steps):
-            ctx.step((f + k) / 60.0)
-        ka, _ = ctx.kernel_stats(0)
-        kb, _ = ctx.kernel_stats(1)
-        km, nm = ctx.kernel_stats(2)
-        ctx.set_kernel_timing(False)
-        mips_sym = ctx.kernel_name(2)
-        # the loop: warm-up by time, then `steps` timed Update frames
-        f = 0
-        w0 = time.perf_counter()
-        while f < max(warmup, 2 * len(wb._ring)) or time.perf_counter() - w0 < UPDATE_WARM_S:
-            wb.Update(f / 60.0)
-            f += 1
-        wb.WaitForReadback()
-        warm_frames, warm_s = f, time.perf_counter() - w0
-        wb.readback_copy_ms = []
-        t0 = time.perf_counter()
-        for k in range(steps):
-            wb.Update((f + k) / 60.0)
-        wb.WaitForReadback()  # every requested readback has landed inside the timed region
-        loop_s = (time.perf_counter() - t0) / steps
-        copies = list(wb.readback_copy_ms)
-        wb.readback_copy_ms = None
-        # the same loop again with the frame's kernels timed (HIP events): are the frames stretched by
-        # the copies beside them?
-        ctx.set_kernel_timing(True)
-        ctx.kernel_stats(0), ctx.kernel_stats(1), ctx.kernel_stats(2)
-        for k in range(steps):
-            wb.Update((f + steps + k) / 60.0)
-        wb.WaitForReadback()
-        la, _ = ctx.kernel_stats(0)
-        lb, _ = ctx.kernel_stats(1)
-        lm, _ = ctx.kernel_stats(2)
-        ctx.set_kernel_timing(False)
-        slice_bytes = 1024 * 1024 * 16
-        mips_rec = mip_record()
-        copy_ms = float(np.median(copies)) if copies else None
-        numa = numa_placement(wb.device, [b.ptr.value for b in wb._ring])
-        return {"workload": "cfg3 (4 x 1024^2) frame + GenerateMips of DERIV and TURB + AsyncGPUReadback of "
-                            "DISP slice 0 every frame, ocean_hip.WaterBody.Update (WaterBody.cs:284-297)",
-                "frames_per_s": round(1.0 / loop_s, 2), "ms_per_frame": round(1e3 * loop_s, 4),
-                "timed_frames": steps, "warmup": {"frames": warm_frames, "seconds": round(warm_s, 3)},
-                "pcie_bytes_per_frame": slice_bytes, "pcie_GBs": round(slice_bytes / loop_s / 1e9, 2),
-                "readback_ring_slots": wb._in_flight(),
-                "d2h": {"copies": len(copies), "median_ms": round(copy_ms, 4) if copy_ms else None,
-                        "max_ms": round(max(copies), 4) if copies else None,
-                        "GBs": round(slice_bytes / (copy_ms * 1e-3) / 1e9, 2) if copy_ms else None,
-                        "how": "ocean_readback_copy_ms: HIP events on the copy stream around each device-to-host copy"},
-                "kernel_us_in_loop": {"pass_a": round(1e3 * la / steps, 2), "pass_b": round(1e3 * lb / steps, 2),
-                                      "mips": round(1e3 * lm / steps, 2)},
-                "numa": numa,
-                "step_with_mips": {"frames_per_s": round(1.0 / step_s, 2), "ms_per_frame": round(1e3 * step_s, 4),
-                                   "kernel_us": {"pass_a": round(1e3 * ka / steps, 2), "pass_b": round(1e3 * kb / steps, 2),
-                                                 "mips": round(1e3 * km / steps, 2)},
-                                   "mip_launches_per_frame": nm / steps, "mips_symbol_last": mips_sym,
-                                   "mips_rocprof": mips_rec}}
-    finally:
-        wb.OnDisable()
+                t0 = time.perf_counter()
+                for k in range(steps):
+                    ctx.step((f + k) / 60.0)
+                ctx.synchronize()
+                step_s = (time.perf_counter() - t0) / steps
+                ctx.set_kernel_timing(True)
+                ctx.kernel_stats(0), ctx.kernel_stats(1), ctx.kernel_stats(2)
+                for k in range(steps):
+                    ctx.step((f + k) / 60.0)
+                ka, _ = ctx.kernel_stats(0)
+                kb, _ = ctx.kernel_stats(1)
+                km, nm = ctx.kernel_stats(2)
+                ctx.set_kernel_timing(False)
+                out["step_with_mips"] = {"frames_per_s": round(1.0 / step_s, 2), "ms_per_frame": round(1e3 * step_s, 4),
+                                         "kernel_us": {"pass_a": round(1e3 * ka / steps, 2), "pass_b": round(1e3 * kb / steps, 2),
+                                                       "mips": round(1e3 * km / steps, 2)},
+                                         "mip_launches_per_frame": nm / steps, "mips_symbol_last": ctx.kernel_name(2),
+                                         "mips_rocprof": mip_record()}
+                out["readback_ring_slots"] = wb._in_flight()
+                out["numa"] = numa_placement(wb.device, [b.ptr.value for b in wb._ring])
+            out[mode], _ = _loop_mode(wb, steps, warmup, 0)
+        finally:
+            wb.OnDisable()
+    out["height_over_rgba"] = round(out["height"]["frames_per_s"] / out["rgba"]["frames_per_s"], 3)
+    # top-level figures of the facade's default mode (height)
+    out["frames_per_s"], out["ms_per_frame"] = out["height"]["frames_per_s"], out["height"]["ms_per_frame"]
+    return out
 
 
 def cpu_baseline(cfg, frames=3):

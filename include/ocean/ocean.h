@@ -55,8 +55,11 @@ extern "C" {
  *      ocean_read_async family, ocean_host_alloc/free, ocean_generate_noise_device,
  *      ocean_kernel_name, ocean_set_column_parity.
  *   3  semantics changed: no call moves the calling thread's current HIP device any more
- *      (Conventions).  New: ocean_readback_copy_ms. */
-#define OCEAN_ABI_VERSION 3
+ *      (Conventions).  New: ocean_readback_copy_ms.
+ *   4  semantics changed: ocean_readback_copy_ms needs a request made with readback timing on
+ *      (ocean_set_readback_timing; off by default, so a host that never asks for copy times
+ *      records no timing events).  New: ocean_read_height_async, ocean_set_readback_timing. */
+#define OCEAN_ABI_VERSION 4
 
 /* status codes */
 #define OCEAN_OK 0
@@ -300,10 +303,26 @@ int ocean_read_async(ocean_ctx *ctx, int texture, int tile, int cascade, void *d
 int ocean_readback_status(ocean_readback *rb);
 int ocean_readback_wait(ocean_readback *rb);
 void ocean_readback_release(ocean_readback *rb);
+/* Height-only readback for buoyancy: the reference reads displacement slice 0 back every frame
+ * (WaterBody.cs:288-296) into its private buoyancyData (:58), whose only reader, GetWaterHeight,
+ * returns the .g channel alone (:195-209).  This request copies just that channel, DISP.y = Dy of one
+ * (tile, cascade) slice, as float[N][N] laid out [y][x] (`bytes` = N*N*4: a quarter of the RGBA
+ * slice over the link), with ocean_read_async's snapshot and completion semantics: the same
+ * ocean_readback_status / _wait / _release / _copy_ms apply.  dst[y*N + x] is bit-identical to
+ * the .y of texel (x, y) of the RGBA slice read at the same point of the stream. */
+int ocean_read_height_async(ocean_ctx *ctx, int tile, int cascade, float *dst, size_t bytes,
+                            ocean_readback **out);
+
+/* Readback timing (off after ocean_create): while on, each new ocean_read_async /
+ * ocean_read_height_async request records HIP timing events around its device-to-host copy, for
+ * ocean_readback_copy_ms.  Requests made while it is off record only untimed events. */
+int ocean_set_readback_timing(ocean_ctx *ctx, int enable);
+
 /* Duration of a completed request's device-to-host copy in ms (HIP events on the copy stream around
  * the copy itself: the link's share of the request, without the wait for the queued frames or the
- * on-device snapshot).  OCEAN_E_STATE while the request is pending.  No reference counterpart:
- * AsyncGPUReadback exposes no timing; hosts use it to attribute a readback-bound loop. */
+ * on-device snapshot).  OCEAN_E_STATE while the request is pending, or if it was made with readback
+ * timing off.  No reference counterpart: AsyncGPUReadback exposes no timing; hosts use it to
+ * attribute a readback-bound loop. */
 int ocean_readback_copy_ms(ocean_readback *rb, float *ms);
 
 /* Pinned host memory for ocean_read_async destinations (hipHostMalloc). */

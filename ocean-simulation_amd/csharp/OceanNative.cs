@@ -50,6 +50,7 @@ namespace OceanHip
 
     public static class OceanNative
     {
+        public const int AbiVersion = 4;  // OCEAN_ABI_VERSION of the header this binding follows
         const string Lib = "oceanhip";  // liboceanhip.so next to the managed assembly / on LD_LIBRARY_PATH
 
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
@@ -116,6 +117,10 @@ namespace OceanHip
         public static extern void ocean_readback_release(IntPtr request);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
         public static extern OceanStatus ocean_readback_copy_ms(IntPtr request, out float ms);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
+        public static extern OceanStatus ocean_read_height_async(IntPtr ctx, int tile, int cascade, IntPtr dst, UIntPtr bytes, out IntPtr request);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
+        public static extern OceanStatus ocean_set_readback_timing(IntPtr ctx, int enable);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]
         public static extern OceanStatus ocean_host_alloc(UIntPtr bytes, out IntPtr ptr);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]

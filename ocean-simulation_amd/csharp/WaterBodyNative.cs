@@ -14,6 +14,11 @@ namespace OceanHip
         public float wavelength = 10.0f, cutoffHigh = 5.0f, cutoffLow = 0.0001f, swell = 0.4f, fade = 0.1f;
     }
 
+    // What Update reads back every frame (ocean.h ocean_read_height_async): the height channel alone,
+    // all GetWaterHeight reads (the reference's buoyancyData is private, WaterBody.cs:58, and .g is its
+    // only use, :208), or the whole RGBA displacement slice as the reference requests it.
+    public enum Readback { Height, Rgba }
+
     public sealed class WaterBodyNative : IDisposable
     {
         // Ocean parameters (WaterBody.cs:10-14) and texture size (:29)
@@ -26,15 +31,18 @@ namespace OceanHip
         public WaterCascadeDesc[] cascades = { new WaterCascadeDesc() };
         public int device = 0;
         public ulong seed = 20251121;   // the reference's UnityEngine.Random is unseeded; this library's generator is
+        public Readback readback = Readback.Height;  // set before Awake
 
         IntPtr ctx = IntPtr.Zero;
-        float[] buoyancyData;           // displacement slice 0, RGBA fp32 [y][x] (WaterBody.cs:58, :295)
+        float[] buoyancyData;           // displacement slice 0 (WaterBody.cs:58, :295): [y][x] heights, or RGBA [y][x][4]
+        int Floats => texturesSize * texturesSize * (readback == Readback.Height ? 1 : 4);  // per readback slice
 
         public void Awake()
         {
-            // the rules this facade relies on (ocean.h: ABI 3, no call moves the caller's current device)
-            if (OceanNative.ocean_abi_version() != 3)
-                throw new InvalidOperationException("liboceanhip ABI " + OceanNative.ocean_abi_version() + ", expected 3");
+            // the rules this facade relies on (ocean.h: ABI 4, no call moves the caller's current device)
+            if (OceanNative.ocean_abi_version() != OceanNative.AbiVersion)
+                throw new InvalidOperationException("liboceanhip ABI " + OceanNative.ocean_abi_version() + ", expected " +
+                                                    OceanNative.AbiVersion);
             OceanNative.Check(OceanNative.ocean_create(device, texturesSize, cascades.Length, 1, OceanFlags.Mips, out ctx),
                               "ocean_create");
             ApplyParams();
@@ -43,7 +51,7 @@ namespace OceanHip
             // readback ring: MaxReadbacksInFlight pinned slices allocated once, reused by every
             // request and freed only in Dispose (hipHostFree synchronizes the device: a free per
             // request would make each Update wait for the frame it just queued)
-            int bytes = texturesSize * texturesSize * 4 * sizeof(float);
+            int bytes = Floats * sizeof(float);
             for (int i = 0; i < MaxReadbacksInFlight; i++)
             {
                 OceanNative.Check(OceanNative.ocean_host_alloc((UIntPtr)bytes, out var b), "ocean_host_alloc");
@@ -90,7 +98,7 @@ namespace OceanHip
 
         void Complete((IntPtr req, IntPtr buf) r, bool wait)
         {
-            int n = texturesSize * texturesSize * 4;
+            int n = Floats;
             int st = wait ? (OceanNative.ocean_readback_wait(r.req) == OceanStatus.Ok ? 1 : -1)
                           : OceanNative.ocean_readback_status(r.req);
             if (st == 1)
@@ -108,11 +116,13 @@ namespace OceanHip
             while (readbacks.Count > 0 && OceanNative.ocean_readback_status(readbacks.Peek().req) != 0)
                 Complete(readbacks.Dequeue(), false);
             if (idle.Count == 0) Complete(readbacks.Dequeue(), true);  // every slot in flight: wait for the oldest
-            int n = texturesSize * texturesSize * 4;
             var buf = idle.Pop();
-            var st = OceanNative.ocean_read_async(ctx, OceanTexture.Displacement, 0, 0, buf,
-                                                  (UIntPtr)(n * sizeof(float)), out var req);
-            if (st != OceanStatus.Ok) { idle.Push(buf); OceanNative.Check(st, "ocean_read_async"); }
+            var bytes = (UIntPtr)(Floats * sizeof(float));
+            IntPtr req;
+            var st = readback == Readback.Height
+                         ? OceanNative.ocean_read_height_async(ctx, 0, 0, buf, bytes, out req)
+                         : OceanNative.ocean_read_async(ctx, OceanTexture.Displacement, 0, 0, buf, bytes, out req);
+            if (st != OceanStatus.Ok) { idle.Push(buf); OceanNative.Check(st, "readback request"); }
             readbacks.Enqueue((req, buf));
         }
 
@@ -130,7 +140,8 @@ namespace OceanHip
             float v = InverseLerp(-texturesSize / 2, texturesSize / 2, worldZ);
             int x = Math.Clamp((int)(u * texturesSize), 0, texturesSize - 1);
             int y = Math.Clamp((int)(v * texturesSize), 0, texturesSize - 1);
-            return buoyancyData[(y * texturesSize + x) * 4 + 1];  // .g = Dy
+            int t = y * texturesSize + x;
+            return readback == Readback.Height ? buoyancyData[t] : buoyancyData[t * 4 + 1];  // .g = Dy
         }
 
         // What Water.shader reads at world positions (Water.shader:314-348): points are

@@ -6,6 +6,8 @@
 //   levels 1..5 of that block through LDS (each level 0 texel read once).
 // k_mips_tail: one workgroup per slice builds the remaining levels from level 5.
 // Bytes per texel-cascade: read DERIV + TURB (32 B), write 1/3 of that.
+#include <algorithm>
+
 #include "ocean_internal.h"
 
 namespace ocean {
@@ -80,7 +82,26 @@ __global__ __launch_bounds__(256) void k_mips_tail(DevView v, int first) {
     }
 }
 
+// The height channel (.y = Dy, what GetWaterHeight reads: WaterBody.cs:208) of one DISP slice, compacted
+// to float[N][N] for ocean_read_height_async: a quarter of the RGBA slice's bytes over the link.  Four
+// texels per lane: 64 B read, 16 B written.
+__global__ __launch_bounds__(256) void k_extract_height(const float4* __restrict__ src, float4* __restrict__ dst,
+                                                        size_t quads) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < quads; i += (size_t)gridDim.x * blockDim.x) {
+        const float4 a = src[4 * i], b = src[4 * i + 1], c = src[4 * i + 2], d = src[4 * i + 3];
+        dst[i] = make_float4(a.y, b.y, c.y, d.y);
+    }
+}
+
 }  // namespace
+
+hipError_t launch_extract_height(const float4* disp_slice, float* dst, size_t texels, hipStream_t s) {
+    if (texels % 4 != 0) return hipErrorInvalidValue;
+    const size_t quads = texels / 4;
+    const int g = (int)std::min<size_t>((quads + 255) / 256, 4096);
+    launch(k_extract_height, dim3(g), dim3(256), 0, s, disp_slice, reinterpret_cast<float4*>(dst), quads);
+    return hipGetLastError();
+}
 
 hipError_t launch_mips(const DevView& v, hipStream_t s) {
     if (!v.deriv_mips || !v.turb_mips) return hipErrorInvalidValue;

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "fft_core.h"
+#include "device_scope.h"
 #include "ocean_internal.h"
 
 namespace {
@@ -97,39 +98,62 @@ namespace ocean {
 void generate_noise_host(int n, uint64_t seed, float* out);
 }
 
-// Device staging slots of ocean_read_async, each as large as one slice of the largest texture.  A
-// request takes a slot and gives it back when it is released (after its host copy has landed), so a
-// slot is never rewritten while a copy out of it is pending, and no allocation or free sits between
-// the context stream and the copy stream.  Shared with the requests: it outlives a context destroyed
-// before its requests are released.
+// Staging slots of ocean_read_async / ocean_read_height_async.  A slot is device memory as large as one
+// slice of the largest texture plus the events of the request holding it, created once with the slot: no
+// event is created per request.  `after` and `done` disable timing; the timed pair `tstart` / `tdone`
+// (ocean_readback_copy_ms) is created on the slot's first request made with readback timing on
+// (ocean_set_readback_timing) and recorded only for such requests.  A request takes a slot and gives it back
+// when it is released (after its host copy has landed), so a slot is never rewritten while a copy out of
+// it is pending, and no allocation or free sits between the context stream and the copy stream.  Shared
+// with the requests: it outlives a context destroyed before its requests are released.
+struct StageSlot {
+    void* mem = nullptr;
+    hipEvent_t after = nullptr;  // the snapshot is in the slot (the copy stream waits for it)
+    hipEvent_t done = nullptr;   // the host copy has landed (untimed requests)
+    hipEvent_t tstart = nullptr, tdone = nullptr;  // timed requests: around the host copy itself
+};
 struct StagePool {
     int device = 0;
     size_t slot_bytes = 0;
     std::mutex mu;
-    std::vector<void*> free_slots, all;
+    std::vector<StageSlot*> free_slots, all;
     ~StagePool() {
         int prev = 0;
         const bool had = hipGetDevice(&prev) == hipSuccess;
         (void)hipSetDevice(device);
-        for (void* p : all) (void)hipFree(p);
+        for (StageSlot* sl : all) {
+            if (sl->mem) (void)hipFree(sl->mem);
+            for (hipEvent_t e : {sl->after, sl->done, sl->tstart, sl->tdone})
+                if (e) (void)hipEventDestroy(e);
+            delete sl;
+        }
         if (had) (void)hipSetDevice(prev);  // the caller's current device is left as it was
     }
-    hipError_t take(void** out) {
+    hipError_t take(bool timed, StageSlot** out) {
         std::lock_guard<std::mutex> lk(mu);
         if (free_slots.empty()) {
-            void* p = nullptr;
-            const hipError_t e = hipMalloc(&p, slot_bytes);
+            StageSlot* sl = new (std::nothrow) StageSlot();
+            if (!sl) return hipErrorOutOfMemory;
+            hipError_t e = hipMalloc(&sl->mem, slot_bytes);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&sl->after, hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&sl->done, hipEventDisableTiming);
+            all.push_back(sl);  // freed with the pool even when incomplete
             if (e != hipSuccess) return e;
-            all.push_back(p);
-            free_slots.push_back(p);
+            free_slots.push_back(sl);
         }
-        *out = free_slots.back();
+        StageSlot* sl = free_slots.back();
+        if (timed && !sl->tstart) {
+            hipError_t e = hipEventCreate(&sl->tstart);
+            if (e == hipSuccess) e = hipEventCreate(&sl->tdone);
+            if (e != hipSuccess) return e;
+        }
         free_slots.pop_back();
+        *out = sl;
         return hipSuccess;
     }
-    void give(void* p) {
+    void give(StageSlot* sl) {
         std::lock_guard<std::mutex> lk(mu);
-        free_slots.push_back(p);
+        free_slots.push_back(sl);
     }
 };
 
@@ -144,6 +168,7 @@ struct ocean_options {
     int c4_bands = 0;       // OCEAN_C4_BANDS: N >= 2048 column passes per (unit, band); 0 = auto
     long op_chunk_mib = 0;  // OCEAN_OP_CHUNK_MIB: MiB of unit-planes per chunk of ocean_ifft2d (0: auto)
     int tile_w = 0;         // OCEAN_TILE_W: column-tile width of the fused path at N = 128..1024 (0: auto)
+    int disp_cached = -1;   // OCEAN_DISP_CACHED: 0 / 1 force pass BQ's DISP store policy (disp_fits_cache); -1 auto
 
     static ocean_options from_env() {
         ocean_options o;
@@ -153,6 +178,7 @@ struct ocean_options {
         if (const char* e = std::getenv("OCEAN_C4_BANDS")) o.c4_bands = std::max(0, std::atoi(e));
         if (const char* e = std::getenv("OCEAN_OP_CHUNK_MIB")) o.op_chunk_mib = std::max(0L, std::atol(e));
         if (const char* e = std::getenv("OCEAN_TILE_W")) o.tile_w = std::max(0, std::atoi(e));
+        if (const char* e = std::getenv("OCEAN_DISP_CACHED")) o.disp_cached = std::strcmp(e, "auto") ? std::atoi(e) != 0 : -1;
         return o;
     }
 };
@@ -188,8 +214,9 @@ struct ocean_ctx {
     float4* deriv_mips = nullptr;  // OCEAN_F_MIPS chains (levels 1..log2 N per slice)
     float4* turb_mips = nullptr;
     size_t mip_chain = 0;
-    hipStream_t copy_stream = nullptr;  // ocean_read_async
-    std::shared_ptr<StagePool> stage_pool;  // ocean_read_async staging slots
+    hipStream_t copy_stream = nullptr;  // ocean_read_async / ocean_read_height_async
+    std::shared_ptr<StagePool> stage_pool;  // their staging slots
+    bool readback_timing = false;           // ocean_set_readback_timing
     // host state.  `params` and the device `casc` are what the kernels run with; set_params
     // only stages new values, which ocean_init_spectrum makes active (ocean.h), so a
     // frame stepped between the two still uses the spectrum's own constants.
@@ -262,32 +289,20 @@ struct ocean_ctx {
 
 namespace {
 
-// Makes a device current for the span of one entry point and gives the calling thread its own
-// current device back on return (ocean.h, "Conventions"): a host that drives several contexts from
-// one thread, or runs torch in the same process, never sees its current device move.  hipSetDevice
-// is called only when the device differs.
-class DeviceScope {
+// The device rule of every entry point (device_scope.h) over the HIP runtime: hipSetDevice only when the
+// device differs, and a failure to set it becomes the call's OCEAN_E_DEVICE.
+struct HipDeviceApi {
+    static int get(int* device) { return (int)hipGetDevice(device); }
+    static int set(int device) { return (int)hipSetDevice(device); }
+};
+class DeviceScope : public ocean::BasicDeviceScope<HipDeviceApi> {
   public:
-    explicit DeviceScope(int device) {
-        if (hipGetDevice(&prev_) != hipSuccess) prev_ = -1;
-        if (prev_ == device) return;
-        const hipError_t e = hipSetDevice(device);
-        if (e != hipSuccess) {
-            status_ = hip_fail(e, "hipSetDevice");
-            return;
-        }
-        restore_ = prev_ >= 0;
+    explicit DeviceScope(int device) : ocean::BasicDeviceScope<HipDeviceApi>(device) {
+        if (error()) status_ = hip_fail((hipError_t)error(), "hipSetDevice");
     }
-    ~DeviceScope() {
-        if (restore_) (void)hipSetDevice(prev_);
-    }
-    DeviceScope(const DeviceScope&) = delete;
-    DeviceScope& operator=(const DeviceScope&) = delete;
     int status() const { return status_; }
 
   private:
-    int prev_ = -1;
-    bool restore_ = false;
     int status_ = OCEAN_OK;
 };
 
@@ -803,13 +818,18 @@ bool use_q(const ocean_ctx* ctx) {
 }
 
 // Pass BQ may write DISP with default-policy stores (DevView::disp_cached) when the whole frame is one chunk
-// and its cache-resident set -- h0k, the three-plane intermediate, the foam state -- plus DISP fits 224 MiB of
-// the 256 MiB Infinity Cache: DISP then waits there and is written back while the next pass A runs, when HBM
-// has headroom.  cfg3 (4 x 1024^2, 208 MiB): 11.83-11.88 -> 12.08-12.11 k frames/s; a cfg4 chunk (32 units of
-// 512^2, 288 MiB) lost 7.5 % the same way, and DISP + TURB at cfg3 lost 7 % (docs/MEASUREMENTS.md section 8).
+// and its cache-resident set plus DISP fits 224 MiB of the 256 MiB Infinity Cache of an MI355X: DISP then
+// waits there and is written back while the next pass A runs, when HBM has headroom.  The resident set is
+// what the three-plane frame re-reads each frame, per texel-cascade: pass AQ's h0k (8 B; the frame runs
+// only with the mirror-pair row pass, use_q), the intermediate Q1..Q3 (24 B) and the foam state (4 B).
+// cfg3 (4 x 1024^2, 208 MiB): 11.83-11.88 -> 12.08-12.11 k frames/s; a cfg4 chunk (32 units of 512^2,
+// 288 MiB) lost 7.5 % the same way, and DISP + TURB at cfg3 lost 7 % (docs/MEASUREMENTS.md section 8).
+// The 224 MiB budget is this part's; OCEAN_DISP_CACHED=0 / 1 overrides the choice (A/B, other parts).
 bool disp_fits_cache(const ocean_ctx* ctx, bool q, int chunk) {
     if (!q || ctx->n > 1024 || chunk < (int)ctx->units()) return false;
-    const size_t bytes = ctx->texels() * ctx->units() * (8 + 24 + 4 + 16);
+    if (ctx->opt.disp_cached >= 0) return ctx->opt.disp_cached != 0;
+    constexpr size_t kH0k = 8, kInter = 24, kFoam = 4, kDisp = 16;
+    const size_t bytes = ctx->texels() * ctx->units() * (kH0k + kInter + kFoam + kDisp);
     return bytes <= ((size_t)224 << 20);
 }
 
@@ -937,18 +957,51 @@ int ocean_get_mip_ptr(ocean_ctx* ctx, int texture, int level, void** ptr, size_t
 }  // extern "C"
 
 struct ocean_readback {
-    hipEvent_t done = nullptr;   // the host copy has landed
-    hipEvent_t after = nullptr;  // the snapshot is in the slot (the copy stream waits for it)
-    hipEvent_t start = nullptr;  // the copy stream reached the host copy (ocean_readback_copy_ms)
     int device = 0;
-    void* slot = nullptr;
+    bool timed = false;  // made with readback timing on: tstart / tdone recorded
+    StageSlot* slot = nullptr;
     std::shared_ptr<StagePool> pool;
+    hipEvent_t done() const { return timed ? slot->tdone : slot->done; }
 };
 
 namespace {
-// The host copy of ocean_read_async: hipMemcpyDeviceToHost (see docs/MEASUREMENTS.md section 8 for the
+// The host copy of the readbacks: hipMemcpyDeviceToHost (see docs/MEASUREMENTS.md section 8 for the
 // engine the runtime picks)
 constexpr hipMemcpyKind kReadbackCopyKind = hipMemcpyDeviceToHost;
+
+// A readback request: `snapshot` enqueues the copy of the wanted bytes into the slot on the ctx stream
+// (ordered after the queued steps and before later ones, at HBM speed), then the host copy runs on the
+// copy stream, off the ctx stream's path -- snapshot semantics, like a readback in Unity's command stream.
+template <class Snapshot>
+int start_readback(ocean_ctx* ctx, void* dst, size_t bytes, Snapshot&& snapshot, ocean_readback** out) {
+    if (!ctx->copy_stream) OCEAN_HIP(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+    if (!ctx->stage_pool) {
+        ctx->stage_pool = std::make_shared<StagePool>();
+        ctx->stage_pool->device = ctx->device;
+        ctx->stage_pool->slot_bytes = ctx->texels() * 16;  // the largest slice (float4 textures)
+    }
+    ocean_readback* rb = new (std::nothrow) ocean_readback();
+    if (!rb) return fail(OCEAN_E_OUT_OF_MEMORY, "host allocation failed");
+    rb->device = ctx->device;
+    rb->pool = ctx->stage_pool;
+    rb->timed = ctx->readback_timing;
+    hipError_t e = rb->pool->take(rb->timed, &rb->slot);
+    if (e == hipSuccess) e = snapshot(rb->slot->mem);
+    if (e == hipSuccess) e = hipEventRecord(rb->slot->after, ctx->stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(ctx->copy_stream, rb->slot->after, 0);
+    if (e == hipSuccess && rb->timed) e = hipEventRecord(rb->slot->tstart, ctx->copy_stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(dst, rb->slot->mem, bytes, kReadbackCopyKind, ctx->copy_stream);
+    if (e == hipSuccess) e = hipEventRecord(rb->done(), ctx->copy_stream);
+    if (e != hipSuccess) {
+        (void)hipStreamSynchronize(ctx->copy_stream);
+        (void)hipStreamSynchronize(ctx->stream);
+        if (rb->slot) rb->pool->give(rb->slot);
+        delete rb;
+        return hip_fail(e, "readback request");
+    }
+    *out = rb;
+    return OCEAN_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -961,46 +1014,39 @@ int ocean_read_async(ocean_ctx* ctx, int texture, int tile, int cascade, void* d
     if (!dst) return fail(OCEAN_E_INVALID_ARG, "null destination");
     char* src = nullptr;
     if (int r = slice_ptr(ctx, texture, tile, cascade, bytes, &src)) return r;
-    if (!ctx->copy_stream) OCEAN_HIP(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
-    if (!ctx->stage_pool) {
-        ctx->stage_pool = std::make_shared<StagePool>();
-        ctx->stage_pool->device = ctx->device;
-        ctx->stage_pool->slot_bytes = ctx->texels() * 16;  // the largest slice (float4 textures)
-    }
-    ocean_readback* rb = new (std::nothrow) ocean_readback();
-    if (!rb) return fail(OCEAN_E_OUT_OF_MEMORY, "host allocation failed");
-    rb->device = ctx->device;
-    rb->pool = ctx->stage_pool;
-    // Snapshot semantics, like a readback in Unity's command stream: a device-side copy into a
-    // staging slot on the ctx stream (ordered after the queued steps and before later ones,
-    // ~16 MiB at HBM speed), then the host copy on the copy stream, off the ctx stream's path.
-    hipError_t e = hipEventCreateWithFlags(&rb->after, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreate(&rb->start);
-    if (e == hipSuccess) e = hipEventCreate(&rb->done);
-    if (e == hipSuccess) e = rb->pool->take(&rb->slot);
-    if (e == hipSuccess) e = hipMemcpyAsync(rb->slot, src, bytes, hipMemcpyDeviceToDevice, ctx->stream);
-    if (e == hipSuccess) e = hipEventRecord(rb->after, ctx->stream);
-    if (e == hipSuccess) e = hipStreamWaitEvent(ctx->copy_stream, rb->after, 0);
-    if (e == hipSuccess) e = hipEventRecord(rb->start, ctx->copy_stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(dst, rb->slot, bytes, kReadbackCopyKind, ctx->copy_stream);
-    if (e == hipSuccess) e = hipEventRecord(rb->done, ctx->copy_stream);
-    if (e != hipSuccess) {
-        (void)hipStreamSynchronize(ctx->copy_stream);
-        (void)hipStreamSynchronize(ctx->stream);
-        if (rb->slot) rb->pool->give(rb->slot);
-        if (rb->done) (void)hipEventDestroy(rb->done);
-        if (rb->start) (void)hipEventDestroy(rb->start);
-        if (rb->after) (void)hipEventDestroy(rb->after);
-        delete rb;
-        return hip_fail(e, "ocean_read_async");
-    }
-    *out = rb;
+    return start_readback(
+        ctx, dst, bytes, [&](void* slot) { return hipMemcpyAsync(slot, src, bytes, hipMemcpyDeviceToDevice, ctx->stream); },
+        out);
+}
+
+int ocean_read_height_async(ocean_ctx* ctx, int tile, int cascade, float* dst, size_t bytes, ocean_readback** out) {
+    if (!out) return fail(OCEAN_E_INVALID_ARG, "out is null");
+    *out = nullptr;
+    OCEAN_ENTER(ctx);
+    if (!dst) return fail(OCEAN_E_INVALID_ARG, "null destination");
+    if (bytes != ctx->texels() * 4)
+        return fail(OCEAN_E_INVALID_ARG, "byte count " + std::to_string(bytes) + " != N * N * 4 = " +
+                                             std::to_string(ctx->texels() * 4));
+    char* src = nullptr;
+    if (int r = slice_ptr(ctx, OCEAN_TEX_DISP, tile, cascade, ctx->texels() * 16, &src)) return r;
+    return start_readback(
+        ctx, dst, bytes,
+        [&](void* slot) {
+            return ocean::launch_extract_height(reinterpret_cast<const float4*>(src), static_cast<float*>(slot),
+                                                ctx->texels(), ctx->stream);
+        },
+        out);
+}
+
+int ocean_set_readback_timing(ocean_ctx* ctx, int enable) {
+    if (!ctx) return fail(OCEAN_E_INVALID_ARG, "null context");
+    ctx->readback_timing = enable != 0;
     return OCEAN_OK;
 }
 
 int ocean_readback_status(ocean_readback* rb) {
     if (!rb) return fail(OCEAN_E_INVALID_ARG, "null readback");
-    const hipError_t e = hipEventQuery(rb->done);
+    const hipError_t e = hipEventQuery(rb->done());
     if (e == hipSuccess) return 1;
     if (e == hipErrorNotReady) return 0;
     return hip_fail(e, "hipEventQuery");
@@ -1008,7 +1054,7 @@ int ocean_readback_status(ocean_readback* rb) {
 
 int ocean_readback_wait(ocean_readback* rb) {
     if (!rb) return fail(OCEAN_E_INVALID_ARG, "null readback");
-    OCEAN_HIP(hipEventSynchronize(rb->done));
+    OCEAN_HIP(hipEventSynchronize(rb->done()));
     return OCEAN_OK;
 }
 
@@ -1016,10 +1062,7 @@ void ocean_readback_release(ocean_readback* rb) {
     if (!rb) return;
     {
         DeviceScope device_scope(rb->device);
-        (void)hipEventSynchronize(rb->done);  // the slot is free only once its host copy has landed
-        (void)hipEventDestroy(rb->done);
-        (void)hipEventDestroy(rb->start);
-        (void)hipEventDestroy(rb->after);
+        (void)hipEventSynchronize(rb->done());  // the slot is free only once its host copy has landed
         rb->pool->give(rb->slot);
     }
     delete rb;
@@ -1027,10 +1070,11 @@ void ocean_readback_release(ocean_readback* rb) {
 
 int ocean_readback_copy_ms(ocean_readback* rb, float* ms) {
     if (!rb || !ms) return fail(OCEAN_E_INVALID_ARG, "null readback or output");
-    const hipError_t q = hipEventQuery(rb->done);
+    if (!rb->timed) return fail(OCEAN_E_STATE, "request made without readback timing (ocean_set_readback_timing)");
+    const hipError_t q = hipEventQuery(rb->done());
     if (q == hipErrorNotReady) return fail(OCEAN_E_STATE, "readback still pending");
     if (q != hipSuccess) return hip_fail(q, "hipEventQuery");
-    OCEAN_HIP(hipEventElapsedTime(ms, rb->start, rb->done));
+    OCEAN_HIP(hipEventElapsedTime(ms, rb->slot->tstart, rb->done()));
     return OCEAN_OK;
 }
 

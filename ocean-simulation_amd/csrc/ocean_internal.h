@@ -125,6 +125,8 @@ hipError_t launch_pass_a_v3(const DevView& v, float t, hipStream_t s);
 hipError_t launch_pass_b_v3(const DevView& v, hipStream_t s);
 // mips.hip: box-filter mip chains of DERIV and TURB (OCEAN_F_MIPS)
 hipError_t launch_mips(const DevView& v, hipStream_t s);
+// mips.hip: DISP.y of one slice compacted to float[N][N] (ocean_read_height_async); texels % 4 == 0
+hipError_t launch_extract_height(const float4* disp_slice, float* dst, size_t texels, hipStream_t s);
 // sample.hip: cascade-summed world sampling (Water.shader:314-348), device pointers
 hipError_t launch_sample_world(const DevView& v, int tile, const float* pts, int count, float* out, hipStream_t s);
 

@@ -4,10 +4,11 @@
 // -> OnDisable.  tests/test_gpu_host.py runs it and checks every number it writes
 // against the same sequence through the Python binding and against the oracle.
 //
-//   abi_host <outdir> <n> <cascades> <frames>
+//   abi_host <outdir> <n> <cascades> <frames> [height|rgba]
 //
-// Writes <outdir>/buoyancy0.bin (buoyancyData after the first F frames, float32
-// [n][n][4]), buoyancy1.bin (after OnValidate + one frame), heights.bin (float32
+// The readback mode (water_body.h Readback) defaults to height.  Writes <outdir>/buoyancy0.bin
+// (buoyancyData after the first F frames, float32 [n][n] heights, or [n][n][4] with rgba),
+// buoyancy1.bin (after OnValidate + one frame), heights.bin (float32
 // [F][4]: GetWaterHeight at 4 world points after each Update), sample.bin (float32
 // [8][12], SampleWorld of 8 points) and prints one JSON summary line.
 #include <cstdio>
@@ -30,8 +31,13 @@ void write_bin(const std::string& path, const float* data, size_t count) {
 }  // namespace
 
 int main(int argc, char** argv) {
-    if (argc != 5) {
-        std::fprintf(stderr, "usage: %s <outdir> <n> <cascades> <frames>\n", argv[0]);
+    if (argc != 5 && argc != 6) {
+        std::fprintf(stderr, "usage: %s <outdir> <n> <cascades> <frames> [height|rgba]\n", argv[0]);
+        return 2;
+    }
+    const std::string mode = argc == 6 ? argv[5] : "height";
+    if (mode != "height" && mode != "rgba") {
+        std::fprintf(stderr, "usage: readback mode must be height or rgba\n");
         return 2;
     }
     const std::string out = argv[1];
@@ -52,6 +58,7 @@ int main(int argc, char** argv) {
         wb.texturesSize = n;
         wb.cascades.assign(scene, scene + (C < 4 ? C : 4));
         wb.seed = 42;
+        wb.readback = mode == "height" ? ocean_host::Readback::Height : ocean_host::Readback::Rgba;
         wb.Awake();
         const float probe[4][2] = {{0.0f, 0.0f}, {-(float)n / 2, -(float)n / 2}, {(float)n / 2 - 1, 50.0f}, {500.0f, -500.0f}};
         std::vector<float> heights;

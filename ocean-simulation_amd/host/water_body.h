@@ -24,6 +24,11 @@ inline void check(int rc, const char* where) {
                                                  ocean_last_error());
 }
 
+// What Update reads back every frame: the height channel GetWaterHeight reads (ocean_read_height_async,
+// 4 B per texel; the reference's buoyancyData is private, WaterBody.cs:58, and .g is all its reader uses)
+// or the whole RGBA displacement slice (ocean_read_async, 16 B per texel) as the reference requests it.
+enum class Readback { Height, Rgba };
+
 struct WaterCascade {  // WaterCascade.cs:10-24 (script defaults)
     float wavelength = 10.0f, cutoffHigh = 5.0f, cutoffLow = 0.0001f, swell = 0.4f, fade = 0.1f;
 };
@@ -39,6 +44,7 @@ public:
     int device = 0;
     size_t maxReadbacksInFlight = 4;  // bound on queued requests (set before Awake): 2-4 keep the copies back to
                                       // back beside the frames; 8 stretch each
+    Readback readback = Readback::Height;  // set before Awake
 
     WaterBody() = default;
     WaterBody(const WaterBody&) = delete;
@@ -88,10 +94,12 @@ public:
         Pending p;
         p.buf = free_.back();
         free_.pop_back();
-        const int rc = ocean_read_async(ctx_, OCEAN_TEX_DISP, 0, 0, p.buf, SliceBytes(), &p.req);
+        const int rc = readback == Readback::Height
+                           ? ocean_read_height_async(ctx_, 0, 0, static_cast<float*>(p.buf), SliceBytes(), &p.req)
+                           : ocean_read_async(ctx_, OCEAN_TEX_DISP, 0, 0, p.buf, SliceBytes(), &p.req);
         if (rc != OCEAN_OK) {
             free_.push_back(p.buf);
-            check(rc, "ocean_read_async");
+            check(rc, readback == Readback::Height ? "ocean_read_height_async" : "ocean_read_async");
         }
         readbacks_.push_back(p);
         ++requested_;
@@ -115,7 +123,8 @@ public:
         const float v = inverse_lerp((float)(-n / 2), (float)(n / 2), worldZ);
         const int x = std::min(std::max((int)(u * n), 0), n - 1);
         const int y = std::min(std::max((int)(v * n), 0), n - 1);
-        return held_[((size_t)y * n + x) * 4 + 1];  // .g = Dy
+        const size_t t = (size_t)y * n + x;
+        return readback == Readback::Height ? held_[t] : held_[t * 4 + 1];  // .g = Dy
     }
 
     // What Water.shader reads at world positions (x, z, lod) -> 12 floats per point.
@@ -146,8 +155,8 @@ public:
         ctx_ = nullptr;
     }
 
-    // The last landed displacement slice 0 (WaterBody.cs:295's array); empty before the first
-    // readback lands.  Copied out of its pinned slot once, on the first call after it lands; later
+    // The last landed displacement slice 0 (WaterBody.cs:295's array): [y][x] heights (Readback::Height)
+    // or [y][x][rgba] (Readback::Rgba); empty before the first readback lands.  Copied out of its pinned slot once, on the first call after it lands; later
     // calls return the same array until the next readback lands (the reference reads a field).
     const std::vector<float>& buoyancyData() {
         if (held_ && !buoy_valid_) {
@@ -175,7 +184,7 @@ private:
     bool buoy_valid_ = false;
     long requested_ = 0, completed_ = 0;
 
-    size_t SliceBytes() const { return (size_t)texturesSize * texturesSize * 16; }
+    size_t SliceBytes() const { return (size_t)texturesSize * texturesSize * (readback == Readback::Height ? 4 : 16); }
 
     void ApplyParams() {
         ocean_params p{windSpeed, windDirectionX, windDirectionY, gravity, fetch, depth};

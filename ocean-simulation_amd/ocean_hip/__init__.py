@@ -60,7 +60,7 @@ EXPORTED_SYMBOLS = (
     "ocean_write", "ocean_get_device_ptr", "ocean_get_stream", "ocean_synchronize",
     "ocean_set_kernel_timing", "ocean_kernel_stats", "ocean_step_bytes", "ocean_read_mip", "ocean_get_mip_ptr",
     "ocean_generate_noise_device", "ocean_read_async", "ocean_readback_status", "ocean_readback_wait", "ocean_readback_release",
-    "ocean_readback_copy_ms",
+    "ocean_readback_copy_ms", "ocean_read_height_async", "ocean_set_readback_timing",
     "ocean_host_alloc", "ocean_host_free", "ocean_last_error", "ocean_abi_version", "ocean_set_column_band",
     "ocean_reset_foam", "ocean_sample_world", "ocean_sample_world_device", "ocean_kernel_name",
     "ocean_set_column_parity",
@@ -128,6 +128,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "ocean_readback_wait": ([P], i),
         "ocean_readback_release": ([P], None),
         "ocean_readback_copy_ms": ([P, ctypes.POINTER(f)], i),
+        "ocean_read_height_async": ([P, i, i, P, sz, ctypes.POINTER(P)], i),
+        "ocean_set_readback_timing": ([P, i], i),
         "ocean_host_alloc": ([sz, ctypes.POINTER(P)], i),
         "ocean_host_free": ([P], None),
         "ocean_last_error": ([], ctypes.c_char_p),
@@ -269,6 +271,15 @@ class OceanContext:
         `buf`: a caller-owned pinned slot to land in (else the request allocates its own)."""
         return Readback(self, tex, tile, cascade, buf)
 
+    def read_height_async(self, tile: int = 0, cascade: int = 0, buf: "PinnedBuffer" = None) -> "Readback":
+        """The height-only readback (ocean_read_height_async): DISP.y of one slice as float32[N][N], a
+        quarter of read_async(TEX_DISP)'s bytes -- all GetWaterHeight reads (WaterBody.cs:195-209)."""
+        return Readback(self, TEX_DISP, tile, cascade, buf, height=True)
+
+    def set_readback_timing(self, enable: bool) -> None:
+        """Time each new readback's device-to-host copy (Readback.copy_ms); off after create."""
+        _check(self.lib.ocean_set_readback_timing(self._h, 1 if enable else 0), "ocean_set_readback_timing")
+
     def device_ptr(self, tex: int):
         p, b = ctypes.c_void_p(), ctypes.c_size_t()
         _check(self.lib.ocean_get_device_ptr(self._h, tex, ctypes.byref(p), ctypes.byref(b)), "ocean_get_device_ptr")
@@ -338,13 +349,14 @@ class PinnedBuffer:
 
 
 class Readback:
-    """One ocean_read_async request into pinned host memory: a caller's PinnedBuffer slot, or
-    one of its own (freed by release())."""
+    """One ocean_read_async (or, `height`, ocean_read_height_async) request into pinned host memory:
+    a caller's PinnedBuffer slot, or one of its own (freed by release())."""
 
-    def __init__(self, ctx: "OceanContext", tex: int, tile: int, cascade: int, buf: Optional[PinnedBuffer] = None):
+    def __init__(self, ctx: "OceanContext", tex: int, tile: int, cascade: int, buf: Optional[PinnedBuffer] = None,
+                 height: bool = False):
         self.lib = ctx.lib
-        ch = _TEX_CHANNELS[tex]
-        self.shape = (ctx.n, ctx.n, ch)
+        ch = 1 if height else _TEX_CHANNELS[tex]
+        self.shape = (ctx.n, ctx.n) if height else (ctx.n, ctx.n, ch)
         self.nbytes = ctx.n * ctx.n * ch * 4
         self._h = ctypes.c_void_p()
         self.slot = buf
@@ -355,13 +367,16 @@ class Readback:
             raise ValueError(f"pinned slot of {buf.nbytes} B < slice {self.nbytes} B")
         self._pinned = buf
         self._buf = buf.ptr
-        rc = self.lib.ocean_read_async(ctx._h, tex, tile, cascade, self._buf, self.nbytes, ctypes.byref(self._h))
+        if height:
+            rc = self.lib.ocean_read_height_async(ctx._h, tile, cascade, self._buf, self.nbytes, ctypes.byref(self._h))
+        else:
+            rc = self.lib.ocean_read_async(ctx._h, tex, tile, cascade, self._buf, self.nbytes, ctypes.byref(self._h))
         if rc != OK:
             if self._own:
                 buf.release()
             self._pinned = None
             self._buf = ctypes.c_void_p()
-            _check(rc, "ocean_read_async")
+            _check(rc, "ocean_read_height_async" if height else "ocean_read_async")
 
     def done(self) -> bool:
         rc = self.lib.ocean_readback_status(self._h)
@@ -373,7 +388,8 @@ class Readback:
         _check(self.lib.ocean_readback_wait(self._h), "ocean_readback_wait")
 
     def copy_ms(self) -> float:
-        """The completed request's device-to-host copy duration (ocean_readback_copy_ms)."""
+        """The completed request's device-to-host copy duration (ocean_readback_copy_ms; the request must
+        have been made with readback timing on: OceanContext.set_readback_timing)."""
         ms = ctypes.c_float()
         _check(self.lib.ocean_readback_copy_ms(self._h, ctypes.byref(ms)), "ocean_readback_copy_ms")
         return ms.value
@@ -436,6 +452,10 @@ class WaterBody:
     asynchronously and, once a request completes, refreshes buoyancyData for
     GetWaterHeight (AsyncGPUReadback, WaterBody.cs:284-297, 195-209).
     `tiles` > 1 batches independent oceans (tile k uses seed + k).
+    `readback`: "height" (default) requests only the .g channel GetWaterHeight reads
+    (ocean_read_height_async, 4 B per texel: the reference's buoyancyData is private,
+    WaterBody.cs:58, and that is its only reader); "rgba" requests the whole Color slice
+    (16 B per texel) as the reference does.  GetWaterHeight returns the same bits in both.
     """
     windSpeed: float = 1.0
     windDirection: tuple = (1.0, 1.0)
@@ -451,6 +471,7 @@ class WaterBody:
     mips: bool = True  # WaterBody.cs:228-229 creates DERIV / TURB with mip chains
     device: int = 0
     noise: Optional[np.ndarray] = None  # explicit noise texture (tile 0), float32[N][N][2]
+    readback: str = "height"  # "height" (DISP.y only) or "rgba" (the whole displacement slice)
 
     def __post_init__(self):
         self.ctx: Optional[OceanContext] = None
@@ -461,6 +482,7 @@ class WaterBody:
         self._held: Optional[PinnedBuffer] = None  # the pinned slot the last landed slice stays in
         self._buoy_copy: Optional[np.ndarray] = None  # buoyancyData's copy of the landed slice (first access)
         self.readback_copy_ms: Optional[List[float]] = None  # set to [] to log each landed copy's time
+        self._timed = False  # the context's readback timing (on while readback_copy_ms is a list)
 
     def params(self) -> dict:
         return dict(wind_speed=self.windSpeed, wind_dir_x=self.windDirection[0], wind_dir_y=self.windDirection[1],
@@ -479,7 +501,10 @@ class WaterBody:
         else:
             self.ctx.generate_noise(self.seed)
         self.ctx.init_spectrum()
-        slice_bytes = self.texturesSize * self.texturesSize * 16
+        if self.readback not in ("height", "rgba"):
+            raise ValueError(f"readback must be 'height' or 'rgba', got {self.readback!r}")
+        self._timed = False
+        slice_bytes = self.texturesSize * self.texturesSize * (4 if self.readback == "height" else 16)
         # one slot more than the requests in flight: the one the last landed slice stays in
         self._ring = [PinnedBuffer(slice_bytes) for _ in range(self._in_flight() + 1)]
         self._idle = list(self._ring)
@@ -515,9 +540,17 @@ class WaterBody:
         # when full, wait for the oldest
         while self._readbacks and (len(self._readbacks) >= self._in_flight() or not self._idle):
             self._complete(self._readbacks.pop(0))
+        if (self.readback_copy_ms is not None) != self._timed:  # copy times logged: timed requests
+            self._timed = self.readback_copy_ms is not None
+            self.ctx.set_readback_timing(self._timed)
         slot = self._idle.pop()
         try:
-            self._readbacks.append(self.ctx.read_async(TEX_DISP, 0, 0, slot))
+            if self.readback == "height":
+                rb = self.ctx.read_height_async(0, 0, slot)
+            else:
+                rb = self.ctx.read_async(TEX_DISP, 0, 0, slot)
+            rb.timed = self._timed
+            self._readbacks.append(rb)
         except Exception:
             self._idle.append(slot)
             raise
@@ -530,7 +563,7 @@ class WaterBody:
         # buoyancyData copies it out only when a caller asks (16 MiB of host copy saved per frame
         # at 1024^2).
         view = rb.view()
-        if self.readback_copy_ms is not None:
+        if self.readback_copy_ms is not None and rb.timed:
             self.readback_copy_ms.append(rb.copy_ms())
         slot = rb.slot
         rb.release()
@@ -542,7 +575,8 @@ class WaterBody:
 
     @property
     def buoyancyData(self) -> Optional[np.ndarray]:
-        """The last landed displacement slice 0, [y][x][rgba] (WaterBody.cs:295's array), read-only.
+        """The last landed displacement slice 0 (WaterBody.cs:295's array), read-only: [y][x] heights
+        (.g) with readback "height", [y][x][rgba] with "rgba".
         The slice is copied out of its pinned slot once, on the first access after it lands, and the
         same array is returned until the next readback lands: per-sample indexing costs no copy, as
         reading the reference's field does not."""
@@ -575,7 +609,7 @@ class WaterBody:
         v = inv_lerp(-(n // 2), n // 2, float(worldPosition[2]))
         x = min(max(int(u * n), 0), n - 1)
         y = min(max(int(v * n), 0), n - 1)
-        return float(self._buoy[y, x, 1])
+        return float(self._buoy[y, x] if self.readback == "height" else self._buoy[y, x, 1])
 
     def SampleWorld(self, points, tile: int = 0) -> np.ndarray:
         """What Water.shader reads at world positions (x, z, lod): summed displacement,

@@ -44,7 +44,7 @@ def test_exports_every_header_symbol():
 
 
 def test_abi_version():
-    assert oh.load_library().ocean_abi_version() == 3
+    assert oh.load_library().ocean_abi_version() == 4
 
 
 @pytest.mark.parametrize("n,c,t,code", [(100, 1, 1, oh.E_UNSUPPORTED), (8, 1, 1, oh.E_UNSUPPORTED),

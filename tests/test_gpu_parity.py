@@ -5,6 +5,7 @@ norm-relative error max|gpu - oracle| / max|oracle| <= 1e-5 (north_star: "fp32
 outputs within 1e-5 relative"); integer-exact quantities (noise, wave numbers,
 omega) bit-exact.  Run with `python -m pytest tests -m gpu` on an MI355X.
 """
+import ctypes
 import json
 import os
 
@@ -551,8 +552,13 @@ def test_foam_state_resume_via_write():
 
 
 # ----------------------------------------------------------- host mirror
-def test_water_body_facade_and_get_water_height():
-    wb = oh.scene_water_body(n=256, n_cascades=3, seed=42).Awake()
+@pytest.mark.parametrize("mode", ["height", "rgba"])
+def test_water_body_facade_and_get_water_height(mode):
+    """The facade in both readback modes: buoyancyData is the landed slice's .g ([N][N], "height", the
+    default) or the whole RGBA slice ("rgba"); GetWaterHeight reads .g either way."""
+    def sl(d):
+        return d[..., 1] if mode == "height" else d
+    wb = oh.scene_water_body(n=256, n_cascades=3, seed=42, readback=mode).Awake()
     wb.Update(1.5)            # steps and requests slice 0 asynchronously (AsyncGPUReadback)
     wb.WaitForReadback()
     disp = wb.DisplacementsTextures()
@@ -573,25 +579,63 @@ def test_water_body_facade_and_get_water_height():
     # the landed slice stays in its pinned slot (no copy per frame); buoyancyData is a copy the
     # caller owns, as ToArray() gives: more frames than the ring holds leave a kept copy unchanged
     kept = wb.buoyancyData
-    at_16 = wb.ctx.read(oh.TEX_DISP, 0, 0)
+    at_16 = sl(wb.ctx.read(oh.TEX_DISP, 0, 0))
     np.testing.assert_array_equal(kept, at_16)
     for k in range(3 * wb.MAX_READBACKS_IN_FLIGHT):
         wb.Update(2.0 + k / 60.0)
     wb.WaitForReadback()
     last = wb.ctx.read(oh.TEX_DISP, 0, 0)
-    np.testing.assert_array_equal(wb.buoyancyData, last)
+    np.testing.assert_array_equal(wb.buoyancyData, sl(last))
     assert wb.GetWaterHeight((3.0, 0.0, -7.0)) == last[121, 131, 1]  # world (3, -7) -> texel (131, 121)
-    assert not np.array_equal(kept, last)
+    assert not np.array_equal(kept, sl(last))
     np.testing.assert_array_equal(kept, at_16)
     wb.OnDisable()
     assert wb.GetWaterHeight((3.0, 0.0, -7.0)) == last[121, 131, 1]  # the slice outlives the ring
     # 16 MiB slices queue faster than they land: the ring fills before the first request completes
-    big = oh.scene_water_body(n=1024, n_cascades=1, seed=7).Awake()
+    big = oh.scene_water_body(n=1024, n_cascades=1, seed=7, readback=mode).Awake()
     for k in range(3 * big.MAX_READBACKS_IN_FLIGHT):
         big.Update(k / 60.0)
     big.WaitForReadback()
-    np.testing.assert_array_equal(big.buoyancyData, big.ctx.read(oh.TEX_DISP, 0, 0))
+    np.testing.assert_array_equal(big.buoyancyData, sl(big.ctx.read(oh.TEX_DISP, 0, 0)))
     big.OnDisable()
+
+
+def test_height_readback_matches_rgba():
+    """ocean_read_height_async is DISP.y of the slice bit for bit, at the same point of the stream as an
+    RGBA request (snapshot semantics), for every (tile, cascade); GetWaterHeight of the two facade modes is
+    identical over a readback sequence (WaterBody.cs:195-209, :288-296)."""
+    n, cas = 256, O.SCENE_CASCADES[:3]
+    ctx, _ = make_ctx(n, cas, tiles=2)
+    ctx.step(0.5)
+    reqs = [(ctx.read_height_async(t, c), ctx.read_async(oh.TEX_DISP, t, c)) for t in range(2) for c in range(3)]
+    ctx.step(1.0)  # after the requests: both snapshot the t = 0.5 frame
+    for h, rgba in reqs:
+        hd, rd = h.data, rgba.data
+        assert hd.shape == (n, n) and hd.dtype == np.float32
+        np.testing.assert_array_equal(hd, rd[..., 1])
+        with pytest.raises(oh.OceanError) as ei:  # untimed (readback timing is off by default)
+            h.copy_ms()
+        assert ei.value.code == oh.E_STATE
+        h.release()
+        rgba.release()
+    L, out, buf = ctx.lib, ctypes.c_void_p(), oh.PinnedBuffer(n * n * 16)
+    for tile, c, nbytes in ((0, 0, n * n * 16), (0, 3, n * n * 4), (2, 0, n * n * 4)):
+        assert L.ocean_read_height_async(ctx._h, tile, c, buf.ptr, nbytes, ctypes.byref(out)) == oh.E_INVALID_ARG
+    assert L.ocean_read_height_async(ctx._h, 0, 0, None, n * n * 4, ctypes.byref(out)) == oh.E_INVALID_ARG
+    buf.release()
+    ctx.close()
+    bodies = [oh.scene_water_body(n=512, n_cascades=2, seed=9, readback=m).Awake() for m in ("height", "rgba")]
+    pts = [(-300.0 + 23.7 * i, 0.0, 280.0 - 31.3 * i) for i in range(24)]
+    for f in range(6):
+        for wb in bodies:
+            wb.Update(f / 60.0)
+            wb.WaitForReadback()
+        a = [bodies[0].GetWaterHeight(p) for p in pts]
+        b = [bodies[1].GetWaterHeight(p) for p in pts]
+        assert a == b and any(x != 0.0 for x in a)
+        np.testing.assert_array_equal(bodies[0].buoyancyData, bodies[1].buoyancyData[..., 1])
+    for wb in bodies:
+        wb.OnDisable()
 
 
 def test_state_errors():
@@ -792,6 +836,7 @@ def test_async_readback_matches_read():
     n, cas = 256, O.SCENE_CASCADES
     ctx, _ = make_ctx(n, cas)
     ctx.step(0.5)
+    ctx.set_readback_timing(True)  # ocean_readback_copy_ms needs timed requests (ABI 4)
     reqs = [ctx.read_async(oh.TEX_DISP, 0, c) for c in range(len(cas))]
     reqs.append(ctx.read_async(oh.TEX_TURB, 0, 1))
     ctx.step(1.0)  # after the requests: they snapshot the t = 0.5 frame
