@@ -2,6 +2,8 @@
 foam carried over a re-init, WAVES writes under the fused schedule, bounded kernel-timing
 events.  The reference counterparts are WaterBody.cs's Awake / OnValidate / Update order
 (WaterBody.cs:211-256, :324-337, :284-297)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -153,6 +155,12 @@ def test_caller_device_unchanged():
         dst.release()
         yield None
 
+    # The driver's GPU box has one device, so only (0, 0) runs there and the restore branch is covered on
+    # the CPU instead (tests/test_device_scope.py).  A multi-GPU session sets OCEAN_EXPECT_DEVICES=N: the
+    # cross-device pairs are then required, and fewer devices fail the test instead of passing quietly.
+    expect = int(os.environ.get("OCEAN_EXPECT_DEVICES", "1"))
+    assert torch.cuda.device_count() >= expect, \
+        f"OCEAN_EXPECT_DEVICES={expect} but {torch.cuda.device_count()} device(s) visible"
     pairs = [(0, 0)]
     if torch.cuda.device_count() > 1:
         pairs += [(0, 1), (1, 0)]
