@@ -142,10 +142,16 @@ struct StagePool {
             free_slots.push_back(sl);
         }
         StageSlot* sl = free_slots.back();
-        if (timed && !sl->tstart) {
-            hipError_t e = hipEventCreate(&sl->tstart);
-            if (e == hipSuccess) e = hipEventCreate(&sl->tdone);
-            if (e != hipSuccess) return e;
+        if (timed && !sl->tstart) {  // both timed events, or neither
+            hipEvent_t a = nullptr, b = nullptr;
+            hipError_t e = hipEventCreate(&a);
+            if (e == hipSuccess) e = hipEventCreate(&b);
+            if (e != hipSuccess) {
+                if (a) (void)hipEventDestroy(a);
+                return e;
+            }
+            sl->tstart = a;
+            sl->tdone = b;
         }
         free_slots.pop_back();
         *out = sl;
