@@ -72,6 +72,15 @@ def test_null_context_is_an_error_not_a_crash():
     assert L.ocean_step(None, ctypes.c_float(0.0)) == oh.E_INVALID_ARG
     assert L.ocean_synchronize(None) == oh.E_INVALID_ARG
     L.ocean_destroy(None)  # no-op
+    # ABI 4's entries: validated before any device call
+    out = ctypes.c_void_p()
+    assert L.ocean_set_readback_timing(None, 1) == oh.E_INVALID_ARG
+    assert L.ocean_read_height_async(None, 0, 0, None, 64, ctypes.byref(out)) == oh.E_INVALID_ARG
+    assert L.ocean_read_height_async(None, 0, 0, None, 64, None) == oh.E_INVALID_ARG
+    assert L.ocean_readback_status(None) == oh.E_INVALID_ARG
+    ms = ctypes.c_float()
+    assert L.ocean_readback_copy_ms(None, ctypes.byref(ms)) == oh.E_INVALID_ARG
+    L.ocean_readback_release(None)  # no-op
 
 
 def test_host_mirror_surface_matches_reference():

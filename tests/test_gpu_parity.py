@@ -600,6 +600,23 @@ def test_water_body_facade_and_get_water_height(mode):
     big.OnDisable()
 
 
+@pytest.mark.parametrize("knob", ["0", "1", "auto"])
+def test_disp_cached_knob_bit_identical(knob, monkeypatch):
+    """OCEAN_DISP_CACHED (pass BQ's DISP store policy, read at ocean_create) changes no texel: cfg3's frame
+    with DISP forced nontemporal, forced default-policy and the automatic choice, against the default."""
+    n, cas = 1024, O.SCENE_CASCADES
+    ref, _ = make_ctx(n, cas)
+    monkeypatch.setenv("OCEAN_DISP_CACHED", knob)
+    ctx, _ = make_ctx(n, cas)
+    for t in (0.5, 1.0):
+        ref.step(t)
+        ctx.step(t)
+    for tex in (oh.TEX_DISP, oh.TEX_DERIV, oh.TEX_TURB):
+        np.testing.assert_array_equal(ctx.read_all(tex), ref.read_all(tex))
+    ref.close()
+    ctx.close()
+
+
 def test_height_readback_matches_rgba():
     """ocean_read_height_async is DISP.y of the slice bit for bit, at the same point of the stream as an
     RGBA request (snapshot semantics), for every (tile, cascade); GetWaterHeight of the two facade modes is
