@@ -19,8 +19,6 @@
 // The planes Q1..Q3 (24 B / texel instead of 32) plus the per-unit side arrays d0 and srow are the
 // whole intermediate; pass B forms R[Q4] from R[Q1] on load.  The outputs equal the four-plane
 // frame's in real arithmetic, Nyquist lines included; in fp32 they differ by rounding only.
-#include <type_traits>
-
 #include "fft_engine.h"
 #include "spectrum_math.h"
 
@@ -555,48 +553,6 @@ __global__ __launch_bounds__(N / 4) void k_pass_a3pp(DevView v, float time, int 
     }
 }
 
-// GenerateMips fused into pass BQ (OCEAN_F_MIPS; WaterBody.cs:191-192).  A wave holds 64 / W rows x W columns
-// of outputs at every (m, q) of the last stage: lane l is column l % W and row bit k of the output is bit k of
-// l / W (out_dy is a multiple of 2^ML), so the 2^k x 2^k boxes of mip levels k <= ML = log2(min(W, 64 / W))
-// lie within the wave.  Level k from level k - 1 exactly as launch_mips's box (mips.hip):
-// ((a + b) + (c + d)) * 0.25 with a, b the two columns of the upper row -- as lane sums, s = own + column
-// neighbour, then s + the row neighbour's s; fp addition commutes, so every lane of the box holds the same bits.
-constexpr int mip_levels_for(int n, int w) {
-    if (n > 1024 || w > 64) return 0;
-    const int side = w < 64 / w ? w : 64 / w;
-    int k = 0;
-    while ((2 << k) <= side) ++k;
-    return k;
-}
-template <int N>
-constexpr size_t mip_level_off(int level) {  // texels before `level` in a slice's chain (levels 1..log2 N)
-    size_t o = 0;
-    for (int l = 1; l < level; ++l) o += (size_t)(N >> l) * (N >> l);
-    return o;
-}
-// The value of lane l ^ M (M a power of two < 64) without an address register: DPP quad permutes for 1 and 2,
-// ds_swizzle's xor mode within 32 lanes for 4..16, v_permlane32_swap for 32.
-template <int M>
-__device__ __forceinline__ float lane_xor(float x) {
-    const int i = __float_as_int(x);
-    if constexpr (M == 1) {
-        return __int_as_float(__builtin_amdgcn_mov_dpp(i, 0xB1, 0xF, 0xF, false));  // quad_perm [1, 0, 3, 2]
-    } else if constexpr (M == 2) {
-        return __int_as_float(__builtin_amdgcn_mov_dpp(i, 0x4E, 0xF, 0xF, false));  // quad_perm [2, 3, 0, 1]
-    } else if constexpr (M <= 16) {
-        return __int_as_float(__builtin_amdgcn_ds_swizzle(i, 0x1F | (M << 10)));  // and 31, xor M
-    } else {
-        static_assert(M == 32, "lane_xor: masks 1..32");
-        const auto p = __builtin_amdgcn_permlane32_swap(i, i, false, false);  // p[1]: lanes 32..63 moved down
-        return __int_as_float((threadIdx.x & 32) ? p[0] : p[1]);
-    }
-}
-template <int CM, int RM>
-__device__ __forceinline__ float box_lanes(float x) {
-    const float s = x + lane_xor<CM>(x);
-    return (s + lane_xor<RM>(s)) * 0.25f;
-}
-
 // Pass BQ: per (unit, W-column tile), four column transforms from three planes:
 //   step 0: R[Q2] -> (Dy, Dyx)          kept (LDS)
 //   step 1: R[Q1] -> (Dx, Dz)           DISP = (Dx, Dy, Dz, 1); Dyx moves to registers; before the
@@ -606,7 +562,7 @@ __device__ __forceinline__ float box_lanes(float x) {
 //   step 3: R[Q3] -> (Dyz, Dxx)         foam (Dxx, Dzz, Dxz), TURB, DERIV = (Dyx, Dyz, Dxx, Dzz)
 // Three tile loads per item run through a three-slot register ring (two steps ahead), as in
 // k_pass_b3; d0 is staged through LDS.  DC (DevView::disp_cached): DISP with default-policy stores.
-template <int N, bool BAND = false, int WT = 0, bool DC = false, int ML = 0>
+template <int N, bool BAND = false, int WT = 0, bool DC = false>
 __global__ __launch_bounds__((WT ? WT : b3_w(N)) * N / kElems) void k_pass_bq(DevView v, int items) {
     using CT = ColTile<N, WT ? WT : b3_w(N)>;
     using E = typename CT::E;
@@ -616,8 +572,6 @@ __global__ __launch_bounds__((WT ? WT : b3_w(N)) * N / kElems) void k_pass_bq(De
     constexpr int RL = CT::RL;
     constexpr int TILE = W * N;
     constexpr bool kKeepLds = (E::LDS_ELEMS + TW::kLdsEntries + kElems * T + N) * 8 <= 160 * 1024;
-    static_assert(ML == 0 || (!BAND && ML <= mip_levels_for(N, W) && (T / W) % (1 << ML) == 0 &&
-                              (N / RL) % (1 << ML) == 0), "fused mips: the boxes lie within a wave");
     __shared__ float2 lds[E::LDS_ELEMS];
     __shared__ float2 twl[TW::kLdsEntries];
     __shared__ float2 keep_lds[kKeepLds ? kElems * T : 1];
@@ -734,29 +688,6 @@ __global__ __launch_bounds__((WT ? WT : b3_w(N)) * N / kElems) void k_pass_bq(De
                     gstore4_nt(make_float4(f, f, f, f), wt, voff16, so);
                     gstore4_nt(make_float4(kreg[i], re, im, k.y), wv, voff16, so);
                     if (v.normals) gstore4_nt(normal_from_deriv(kreg[i], re, im, k.y), win16(v.normal, ft), voff16, so);
-                    if constexpr (ML > 0) {  // mip levels 1..ML of DERIV and TURB (see mip_levels_for)
-                        float4 dm = make_float4(kreg[i], re, im, k.y);
-                        float fm = f;
-                        const int y = lj + dy, xg = x0 + lb;
-                        auto level = [&](auto lev_c) {
-                            constexpr int LEV = decltype(lev_c)::value;
-                            if constexpr (LEV <= ML) {
-                                constexpr int CM = 1 << (LEV - 1), RM = W << (LEV - 1), MSK = (1 << LEV) - 1;
-                                dm = make_float4(box_lanes<CM, RM>(dm.x), box_lanes<CM, RM>(dm.y), box_lanes<CM, RM>(dm.z),
-                                                 box_lanes<CM, RM>(dm.w));
-                                fm = box_lanes<CM, RM>(fm);
-                                if ((lb & MSK) == 0 && (y & MSK) == 0) {
-                                    const size_t o = (size_t)u * v.mip_chain + mip_level_off<N>(LEV) +
-                                                     (size_t)(y >> LEV) * (N >> LEV) + (xg >> LEV);
-                                    v.deriv_mips[o] = dm;
-                                    v.turb_mips[o] = make_float4(fm, fm, fm, fm);
-                                }
-                            }
-                        };
-                        level(std::integral_constant<int, 1>{});
-                        level(std::integral_constant<int, 2>{});
-                        level(std::integral_constant<int, 3>{});
-                    }
                 }
             };
             E::run_regs(cur, lds, tws, emit);
@@ -820,7 +751,7 @@ hipError_t go_a3q(const DevView& v, float t, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <int N, bool BAND = false, int WT = 0, bool DC = false, int ML = 0>
+template <int N, bool BAND = false, int WT = 0, bool DC = false>
 hipError_t go_bq(const DevView& v, hipStream_t s) {
     if constexpr (WT == 0) {
         if (v.tile_w != inter_w(N)) return go_bq<N, BAND, 4, DC>(v, s);
@@ -832,22 +763,10 @@ hipError_t go_bq(const DevView& v, hipStream_t s) {
         if (v.disp_cached) return go_bq<N, BAND, WT, true>(v, s);
     }
     constexpr int W = WT ? WT : b3_w(N);
-    if constexpr (!BAND && ML == 0) {
-        if (v.mip_fused) {
-            constexpr int L = mip_levels_for(N, W);
-            if constexpr (L > 0) {
-                if (v.mip_fused != L) return hipErrorInvalidValue;
-                return go_bq<N, BAND, WT, DC, L>(v, s);
-            } else {
-                return hipErrorInvalidValue;
-            }
-        }
-    }
-    if (BAND && v.mip_fused) return hipErrorInvalidValue;  // a column band has no mip chains (ocean.h)
     constexpr int T = W * N / kElems;
     const int items = v.units * (v.nx / W);
-    const int g = grid_q(k_pass_bq<N, BAND, WT, DC, ML>, T, items);
-    launch((k_pass_bq<N, BAND, WT, DC, ML>), dim3(g), dim3(T), 0, s, v, items);
+    const int g = grid_q(k_pass_bq<N, BAND, WT, DC>, T, items);
+    launch((k_pass_bq<N, BAND, WT, DC>), dim3(g), dim3(T), 0, s, v, items);
     return hipGetLastError();
 }
 
@@ -856,8 +775,6 @@ hipError_t go_bq(const DevView& v, hipStream_t s) {
 // N = 2048 keeps the four-plane passes: pass A3Q's idle fourth sequence slot costs more there
 // than the column passes save (4 x 2048^2: 612 against 599 us per frame; docs/MEASUREMENTS.md section 3).
 bool pass_q_supported(int n, int planes) { return planes == 4 && (n == 512 || n == 1024 || n == 4096); }
-
-int bq_mip_levels(int n, int w) { return mip_levels_for(n, w); }
 
 hipError_t launch_pass_a_q(const DevView& v, float t, hipStream_t s) {
     if (!pass_q_supported(v.n, v.planes) || !v.qside) return hipErrorInvalidValue;

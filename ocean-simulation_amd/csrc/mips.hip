@@ -26,29 +26,27 @@ __device__ __forceinline__ size_t mip_off(int n, int level) {  // texels before 
     return o;
 }
 
-// grid: (blocks per slice, slices, 2 textures); 256 lanes.  Builds levels from + 1 .. from + levels of the
-// blk x blk blocks of level `from` (0: the texture itself; else that level of the chain, which pass BQ wrote).
-__global__ __launch_bounds__(256) void k_mips_block(DevView v, int from, int blk, int levels) {
+// grid: (blocks per slice, slices, 2 textures); 256 lanes
+__global__ __launch_bounds__(256) void k_mips_block(DevView v, int blk, int levels) {
     const int n = v.n;
-    const int ns = n >> from;  // side of the source level
     const int tex = blockIdx.z;
+    const float4* src = (tex == 0 ? v.deriv : v.turb) + (size_t)blockIdx.y * n * n;
     float4* chain = (tex == 0 ? v.deriv_mips : v.turb_mips) + (size_t)blockIdx.y * v.mip_chain;
-    const float4* src = from == 0 ? (tex == 0 ? v.deriv : v.turb) + (size_t)blockIdx.y * n * n : chain + mip_off(n, from);
-    const int bpr = ns / blk;  // blocks per row
+    const int bpr = n / blk;  // blocks per row
     const int bx = blockIdx.x % bpr, by = blockIdx.x / bpr;
     __shared__ float4 cur[kBlk / 2 * kBlk / 2];
-    // level from + 1: lane t -> texel (t % h, t / h) of the h x h block, h = blk / 2
+    // level 1: lane t -> texel (t % h, t / h) of the h x h level-1 block, h = blk / 2
     int h = blk / 2;
     for (int t = threadIdx.x; t < h * h; t += blockDim.x) {
         const int x = t % h, y = t / h;
         const int X = bx * blk + 2 * x, Y = by * blk + 2 * y;
-        const float4 r = box(src[(size_t)Y * ns + X], src[(size_t)Y * ns + X + 1], src[(size_t)(Y + 1) * ns + X],
-                             src[(size_t)(Y + 1) * ns + X + 1]);
-        const int m = n >> (from + 1);
-        chain[mip_off(n, from + 1) + (size_t)(by * h + y) * m + bx * h + x] = r;
+        const float4 r = box(src[(size_t)Y * n + X], src[(size_t)Y * n + X + 1], src[(size_t)(Y + 1) * n + X],
+                             src[(size_t)(Y + 1) * n + X + 1]);
+        const int m = n >> 1;
+        chain[mip_off(n, 1) + (size_t)(by * h + y) * m + bx * h + x] = r;
         cur[t] = r;
     }
-    for (int level = from + 2; level <= from + levels; ++level) {
+    for (int level = 2; level <= levels; ++level) {
         __syncthreads();
         const int hp = h;
         h >>= 1;
@@ -107,17 +105,15 @@ hipError_t launch_extract_height(const float4* disp_slice, float* dst, size_t te
 
 hipError_t launch_mips(const DevView& v, hipStream_t s) {
     if (!v.deriv_mips || !v.turb_mips) return hipErrorInvalidValue;
-    const int n = v.n, from = v.mip_fused;
-    const int ns = n >> from;  // side of the level the launch starts from
-    if (ns < 2) return hipSuccess;
-    const int blk = ns < kBlk ? ns : kBlk;
+    const int n = v.n;
+    const int blk = n < kBlk ? n : kBlk;
     int levels = 0;
-    while ((1 << levels) < blk) ++levels;  // levels from + 1 .. from + log2(blk) from the block kernel
-    const int bps = (ns / blk) * (ns / blk);
-    launch(k_mips_block, dim3(bps, v.units, 2), dim3(256), 0, s, v, from, blk, levels);
+    while ((1 << levels) < blk) ++levels;  // levels 1..log2(blk) from the block kernel
+    const int bps = (n / blk) * (n / blk);
+    launch(k_mips_block, dim3(bps, v.units, 2), dim3(256), 0, s, v, blk, levels);
     if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
-    if (blk < ns) {
-        launch(k_mips_tail, dim3(v.units, 2), dim3(256), 0, s, v, from + levels + 1);
+    if (blk < n) {
+        launch(k_mips_tail, dim3(v.units, 2), dim3(256), 0, s, v, levels + 1);
         return hipGetLastError();
     }
     return hipSuccess;

@@ -741,22 +741,10 @@ namespace {
 int step_fused(ocean_ctx* ctx, float time);
 bool use_q(const ocean_ctx* ctx);
 
-// Mip levels pass BQ builds itself in the fused frame (ocean_internal.h DevView::mip_fused): the three-plane
-// frame at N <= 1024 over the whole band.  Both the step and generate_mips ask here.
-int fused_mip_levels(const ocean_ctx* ctx) {
-#ifdef OCEAN_NO_FUSED_MIPS  // A/B build: every level from the mips kernel
-    return 0;
-#endif
-    if (!(ctx->flags & OCEAN_F_MIPS) || (ctx->flags & OCEAN_F_UNFUSED) || ctx->n > 1024 || !use_q(ctx)) return 0;
-    if (ctx->band_nx != ctx->n || ctx->col_par >= 0) return 0;
-    return ocean::bq_mip_levels(ctx->n, ctx->tile_w);
-}
-
-// GenerateMips (WaterBody.cs:191-192) when the context has mip chains: the levels pass BQ did not build.
+// GenerateMips (WaterBody.cs:191-192) when the context has mip chains.
 int generate_mips(ocean_ctx* ctx) {
     if (!(ctx->flags & OCEAN_F_MIPS)) return OCEAN_OK;
-    ocean::DevView v = ctx->view();
-    v.mip_fused = fused_mip_levels(ctx);
+    const ocean::DevView v = ctx->view();
     return timed(ctx, 2, [&] { return ocean::launch_mips(v, ctx->stream); }, "mips");
 }
 }  // namespace
@@ -793,8 +781,6 @@ ocean::DevView sub_view(const ocean::DevView& v, int u0, int nu, bool inter_at_b
     if (v.deriv) s.deriv = v.deriv + off;
     if (v.turb) s.turb = v.turb + off;
     if (v.normal) s.normal = v.normal + off;
-    if (v.deriv_mips) s.deriv_mips = v.deriv_mips + (size_t)u0 * v.mip_chain;
-    if (v.turb_mips) s.turb_mips = v.turb_mips + (size_t)u0 * v.mip_chain;
     return s;
 }
 
@@ -863,7 +849,6 @@ int step_fused(ocean_ctx* ctx, float time) {
         return fail(OCEAN_E_STATE, "a column parity needs the three-plane frame (h0 from ocean_init_spectrum)");
     const int U = (int)ctx->units(), K = std::min(chunk_units(ctx, q ? q_planes(ctx) : ctx->P), (int)ctx->inter_units);
     v.disp_cached = disp_fits_cache(ctx, q, K);
-    v.mip_fused = fused_mip_levels(ctx);
     for (int u0 = 0; u0 < U; u0 += K) {
         const ocean::DevView c = (K >= U) ? v : sub_view(v, u0, std::min(K, U - u0), ctx->inter_units < ctx->units());
         if (q && ctx->n >= 2048) {

@@ -82,10 +82,6 @@ struct DevView {
     // Infinity Cache and is written back while the next pass A runs, when HBM has headroom.  Set by the host
     // where the frame's re-read set plus DISP fits the cache (ocean_abi.cpp disp_fits_cache).
     bool disp_cached;
-    // OCEAN_F_MIPS with the three-plane frame at N <= 1024: pass BQ builds mip levels 1..mip_fused of DERIV and
-    // TURB itself (cross-lane box sums of its own outputs, fftq.hip) and launch_mips starts from level
-    // mip_fused (0: every level from the textures).  Set by the host (ocean_abi.cpp fused_mip_levels).
-    int mip_fused;
 };
 
 struct SpectrumParams {
@@ -127,10 +123,8 @@ hipError_t launch_ifft_fold(const DevView& v, float2* planes, int ups, int part,
 // the column pass (N <= 1024) reads contiguous tiles and the compact foam state.
 hipError_t launch_pass_a_v3(const DevView& v, float t, hipStream_t s);
 hipError_t launch_pass_b_v3(const DevView& v, hipStream_t s);
-// mips.hip: box-filter mip chains of DERIV and TURB (OCEAN_F_MIPS), levels v.mip_fused + 1 .. log2 N
+// mips.hip: box-filter mip chains of DERIV and TURB (OCEAN_F_MIPS)
 hipError_t launch_mips(const DevView& v, hipStream_t s);
-// fftq.hip: mip levels pass BQ builds itself at tile width w (0 where it cannot: N > 1024, w > 64)
-int bq_mip_levels(int n, int w);
 // mips.hip: DISP.y of one slice compacted to float[N][N] (ocean_read_height_async); texels % 4 == 0
 hipError_t launch_extract_height(const float4* disp_slice, float* dst, size_t texels, hipStream_t s);
 // sample.hip: cascade-summed world sampling (Water.shader:314-348), device pointers
