@@ -480,8 +480,9 @@ def update_loop(steps=200, warmup=20):
         finally:
             wb.OnDisable()
     out["height_over_rgba"] = round(out["height"]["frames_per_s"] / out["rgba"]["frames_per_s"], 3)
-    # top-level figures of the facade's default mode (height)
+    # top-level figures of the facades' default mode (height); "rgba" is the reference's own request
     out["frames_per_s"], out["ms_per_frame"] = out["height"]["frames_per_s"], out["height"]["ms_per_frame"]
+    out["top_level_mode"] = "height"
     return out
 
 
