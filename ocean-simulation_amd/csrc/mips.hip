@@ -64,12 +64,17 @@ __global__ __launch_bounds__(256) void k_mips_block(DevView v, int blk, int leve
     }
 }
 
-// grid: (slices, 2 textures); levels first..log2 n from level first-1 in the chain
+// grid: (slices, 2 textures); levels first..log2 n from level first-1 in the chain.  Levels whose source is
+// larger than kBlk x kBlk (N > 1024) are built from the chain in global memory; from the first source that
+// fits, it is read once into LDS and every further level is built there (one global read round trip instead
+// of one per level: 6.28 -> 5.76 us per cfg3 frame, docs/MEASUREMENTS.md section 9).
 __global__ __launch_bounds__(256) void k_mips_tail(DevView v, int first) {
     const int n = v.n;
     const int tex = blockIdx.y;
     float4* chain = (tex == 0 ? v.deriv_mips : v.turb_mips) + (size_t)blockIdx.x * v.mip_chain;
-    for (int level = first; (n >> level) >= 1; ++level) {
+    __shared__ float4 lv[2][kBlk * kBlk];  // ping-pong images of consecutive levels
+    int level = first;
+    for (; (n >> (level - 1)) > kBlk; ++level) {  // source too large for the LDS image
         const int m = n >> level, mp = n >> (level - 1);
         const float4* s = chain + mip_off(n, level - 1);
         float4* d = chain + mip_off(n, level);
@@ -79,6 +84,26 @@ __global__ __launch_bounds__(256) void k_mips_tail(DevView v, int first) {
                        s[(2 * y + 1) * mp + 2 * x + 1]);
         }
         __syncthreads();
+    }
+    int mp = n >> (level - 1);
+    const float4* s0 = chain + mip_off(n, level - 1);
+    for (int t = threadIdx.x; t < mp * mp; t += blockDim.x) lv[0][t] = s0[t];
+    int cur = 0;
+    for (; (n >> level) >= 1; ++level) {
+        __syncthreads();
+        const int m = n >> level;
+        const float4* src = lv[cur];
+        float4* dst = lv[cur ^ 1];
+        float4* d = chain + mip_off(n, level);
+        for (int t = threadIdx.x; t < m * m; t += blockDim.x) {
+            const int x = t % m, y = t / m;
+            const float4 r = box(src[(2 * y) * mp + 2 * x], src[(2 * y) * mp + 2 * x + 1], src[(2 * y + 1) * mp + 2 * x],
+                                 src[(2 * y + 1) * mp + 2 * x + 1]);
+            dst[t] = r;
+            d[t] = r;
+        }
+        cur ^= 1;
+        mp = m;
     }
 }
 
