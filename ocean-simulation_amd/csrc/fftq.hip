@@ -88,11 +88,7 @@ __device__ __forceinline__ float4 mirror_factors(int x, int y, const WaveBand& w
     const float kmag = sqrtf(kx * kx + kz * kz);
     if (!(kmag >= wb.lo && kmag <= wb.hi)) return make_float4(1.0f, 0.0f, 1.0f, 0.0f);
     const Phase e = evolve_phase(sqrtf(g * kmag), time);
-#ifdef OCEAN_RCP_DIV  // A/B build: the correctly rounded 1 / |k| (tools/pointwise_stages.py)
-    return make_float4(e.ex, e.ey, 1.0f / kmag, 0.0f);
-#else
     return make_float4(e.ex, e.ey, __builtin_amdgcn_rcpf(kmag), 0.0f);
-#endif
 }
 
 // Side arrays of unit u (of the chunk the view covers): d0 [N], then srow [N].

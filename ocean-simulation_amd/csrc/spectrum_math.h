@@ -46,10 +46,6 @@ __device__ __forceinline__ float4 wave_data(int x, int y, int n, WaveBand b, flo
 // to the library sincosf.  ~25 VALU instead of the library's ~45 plus its
 // Payne-Hanek branch.
 __device__ __forceinline__ void sincos_fast(float x, float* s, float* c) {
-#ifdef OCEAN_PHASE_LIBM  // A/B build: the library sincosf everywhere (tools/pointwise_stages.py)
-    sincosf(x, s, c);
-    return;
-#endif
     if (!(fabsf(x) < 131072.0f)) {
         sincosf(x, s, c);
         return;
