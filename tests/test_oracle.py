@@ -302,3 +302,79 @@ def test_sample_world_restatement_known_answers():
     p = np.array([[1.0, 2.0, 1.25]], np.float32)
     o = O.sample_world(disp[:1], deriv[:1], turb[:1], [L], p, deriv_mips=levels, turb_mips=levels)
     np.testing.assert_allclose(o[0, 1], [2.0] * 4, atol=1e-6)
+
+
+def _init_fp32_numpy(n, p, cascades, noise):
+    """InitialSpectrum.compute:33-129 restated in numpy, independently of ocean_oracle.c: every + - * / and sqrt
+    in IEEE fp32 (numpy float32, no contraction) in the shader's operation order, every transcendental as its
+    correctly rounded fp32 value (numpy float64, rounded once) -- the definition DESIGN.md section 2 states."""
+    f = np.float32
+
+    def cr(fn, *a):
+        with np.errstate(all="ignore"):
+            return fn(*[np.asarray(x, np.float64) for x in a]).astype(np.float32)
+
+    PI = f(3.14159265)
+    g, U, F, D = f(p["gravity"]), f(p["wind_speed"]), f(p["fetch"]), f(p["depth"])
+    wdx, wdy = f(p["wind_dir_x"]), f(p["wind_dir_y"])
+    wp = f(22.0) * cr(np.power, np.abs(g * g / (U * F)), f(0.3333))  # :118
+    half = n // 2
+    nz, nx = np.meshgrid(np.arange(n) - half, np.arange(n) - half, indexing="ij")
+    C = len(cascades)
+    h0 = np.zeros((C, n, n, 4), np.float32)
+    with np.errstate(all="ignore"):
+        for c, cs in enumerate(cascades):
+            dk = f(2.0) * PI / f(cs["wavelength"])  # :110
+            kx, kz = nx.astype(np.float32) * dk, nz.astype(np.float32) * dk
+            kmag = np.sqrt(kx * kx + kz * kz)
+            band = (kmag >= f(cs["cutoff_low"])) & (kmag <= f(cs["cutoff_high"]))
+            kangle = cr(np.arctan2, kz, kx)
+            w = np.sqrt(g * kmag)  # :33-35
+            wh = w * np.sqrt(D / g)  # TMA :38-43
+            tma = np.where(wh <= f(1), f(0.5) * wh * wh,
+                           np.where(wh < f(2), f(1) - f(0.5) * (f(2) - wh) * (f(2) - wh), f(1)))
+            alpha = f(0.076) * cr(np.power, np.abs(U * U / (F * g)), f(0.22))  # JONSWAP :47-56
+            sigma = np.where(w <= wp, f(0.07), f(0.09))
+            d = w - wp
+            r = cr(np.exp, -(d * d) / (f(2) * sigma * sigma * wp * wp))
+            jon = alpha * g * g / cr(np.power, w, f(5)) * cr(np.exp, f(-1.25) * cr(np.power, wp / w, f(4))) * \
+                cr(np.power, np.abs(f(3.3)), r)
+            peak_speed = g / wp  # spread power :60-66
+            mu = f(-2.33) - f(1.45) * (U / peak_speed - f(1.17))
+            sp = np.where(w < f(1.05) * wp, f(6.97) * cr(np.power, np.abs(w / wp), f(4.06)),
+                          f(9.77) * cr(np.power, np.abs(w / wp), mu))
+            swell = f(cs["swell"])
+            s = sp + f(16) * cr(np.tanh, w / wp) * swell * swell  # directional spread :78-84
+            s2, s3 = s * s, s * s * s
+            ln2 = cr(np.log, f(2))
+            norm = np.where(s <= f(0.4),
+                            f(0.09) * s3 + (cr(np.power, ln2, f(2)) / PI - PI / f(12)) * s2 + ln2 / PI * s + f(1) / (f(2) * PI),
+                            np.sqrt(s) / (f(2) * np.sqrt(PI)) + f(1) / (f(16) * np.sqrt(PI * s)))  # :69-74
+            ln = np.sqrt(wdx * wdx + wdy * wdy)
+            wtheta = cr(np.arctan2, wdy / ln, wdx / ln)
+            dsp = norm * cr(np.power, np.abs(cr(np.cos, f(0.5) * (kangle - wtheta))), f(2) * s)
+            th = cr(np.tanh, np.minimum(kmag * D, f(20)))  # dw/dk :87-91
+            ch = cr(np.cosh, kmag * D)
+            fd = g * (D * kmag / ch / ch + th) / (w * f(2))
+            fade = cr(np.exp, -f(cs["fade"]) * f(cs["fade"]) * kmag * kmag)  # :95-97
+            amp = np.sqrt(f(2) * tma * jon * dsp * fade * fd / kmag * dk * dk)  # :114-121
+            h0[c, ..., 0] = np.where(band, noise[..., 0] / f(2) * amp, f(0))
+            h0[c, ..., 1] = np.where(band, noise[..., 1] / f(2) * amp, f(0))
+    my = (n - np.arange(n)) % n  # conjugate :135-143
+    mirror = h0[:, my][:, :, my]
+    h0[..., 2] = mirror[..., 0]
+    h0[..., 3] = -mirror[..., 1]
+    return h0
+
+
+@pytest.mark.parametrize("shallow", [False, True])
+def test_init_spectrum_bit_exact_against_numpy_fp32(shallow):
+    """The oracle's initial spectrum equals an independent fp32 restatement bit for bit (fp32 arithmetic in
+    the shader's order, transcendentals correctly rounded), for the scene's four cascades, deep and shallow
+    (every TMA branch)."""
+    n = 64
+    noise = O.generate_noise(n, 20251121)
+    p = O.scene_params(shallow)
+    h0, _ = O.init_spectrum(n, p, O.SCENE_CASCADES, noise)
+    ref = _init_fp32_numpy(n, p, O.SCENE_CASCADES, noise)
+    np.testing.assert_array_equal(h0, ref)
