@@ -38,7 +38,9 @@
  * This restatement is therefore "parity unpinned" by reference-produced
  * vectors; it is cross-checked instead by independent known-answer tests
  * (numpy.fft identity, analytic plane wave, foam recurrence, Hermitian
- * symmetry) and an fp64 numpy restatement -- see tests/test_oracle.py.
+ * symmetry), an fp64 numpy restatement, and fp32 numpy restatements of the
+ * init and of whole frames that it must equal bit for bit -- see
+ * tests/test_oracle.py.
  *
  * Layouts (match the reference's Texture2DArray indexing [slice][y][x]):
  *   noise   float2 [N][N]          texel (x, y) at (y*N + x)*2

@@ -322,6 +322,7 @@ def _init_fp32_numpy(n, p, cascades, noise):
     nz, nx = np.meshgrid(np.arange(n) - half, np.arange(n) - half, indexing="ij")
     C = len(cascades)
     h0 = np.zeros((C, n, n, 4), np.float32)
+    waves = np.zeros((C, n, n, 4), np.float32)
     with np.errstate(all="ignore"):
         for c, cs in enumerate(cascades):
             dk = f(2.0) * PI / f(cs["wavelength"])  # :110
@@ -360,11 +361,12 @@ def _init_fp32_numpy(n, p, cascades, noise):
             amp = np.sqrt(f(2) * tma * jon * dsp * fade * fd / kmag * dk * dk)  # :114-121
             h0[c, ..., 0] = np.where(band, noise[..., 0] / f(2) * amp, f(0))
             h0[c, ..., 1] = np.where(band, noise[..., 1] / f(2) * amp, f(0))
+            waves[c] = np.stack([kx, np.where(band, f(1) / kmag, f(1)), kz, np.where(band, w, f(0))], -1)  # :122-127
     my = (n - np.arange(n)) % n  # conjugate :135-143
     mirror = h0[:, my][:, :, my]
     h0[..., 2] = mirror[..., 0]
     h0[..., 3] = -mirror[..., 1]
-    return h0
+    return h0, waves
 
 
 @pytest.mark.parametrize("shallow", [False, True])
@@ -375,6 +377,107 @@ def test_init_spectrum_bit_exact_against_numpy_fp32(shallow):
     n = 64
     noise = O.generate_noise(n, 20251121)
     p = O.scene_params(shallow)
-    h0, _ = O.init_spectrum(n, p, O.SCENE_CASCADES, noise)
-    ref = _init_fp32_numpy(n, p, O.SCENE_CASCADES, noise)
-    np.testing.assert_array_equal(h0, ref)
+    h0, waves = O.init_spectrum(n, p, O.SCENE_CASCADES, noise)
+    ref_h0, ref_waves = _init_fp32_numpy(n, p, O.SCENE_CASCADES, noise)
+    np.testing.assert_array_equal(h0, ref_h0)
+    np.testing.assert_array_equal(waves, ref_waves)
+
+
+def _libm_fp32():
+    """glibc's fp32 cosf / sinf: the oracle's per-frame phase and twiddle functions (ocean_oracle.c header)."""
+    import ctypes
+    import ctypes.util
+    m = ctypes.CDLL(ctypes.util.find_library("m"))
+    fns = []
+    for name in ("cosf", "sinf"):
+        fn = getattr(m, name)
+        fn.restype, fn.argtypes = ctypes.c_float, [ctypes.c_float]
+        fns.append(np.vectorize(lambda x, fn=fn: fn(float(x)), otypes=[np.float32]))
+    return fns
+
+
+def _frame_fp32_numpy(h0, waves, t, foam, cosf, sinf):
+    """One frame of WaterBody.CalculateWavesTexturesAtTime restated in numpy from the reference's shaders,
+    independently of ocean_oracle.c: evolve (TimeDependentSpectrum.compute:20-47), the radix-2 ping-pong IFFT of
+    each plane (IFFT.compute:37-78 driven by IFFT.cs:24-94: twiddle table, log2N horizontal then log2N vertical
+    steps, permute) and the fill + foam (ResultTexturesFiller.compute:16-34).  fp32 arithmetic in the shaders'
+    order; returns (disp, deriv, turb) as float4[C][N][N] and updates nothing in place."""
+    f = np.float32
+    C, n = h0.shape[0], h0.shape[1]
+    logn = n.bit_length() - 1
+
+    def cmul(ar, ai, br, bi):  # ComplexMult
+        return ar * br - ai * bi, ar * bi + ai * br
+
+    # evolve
+    kx, ik, kz, om = (waves[..., j] for j in range(4))
+    phase = om * f(t)
+    ex, ey = cosf(phase), sinf(phase)
+    ar, ai = cmul(h0[..., 0], h0[..., 1], ex, ey)
+    br, bi = cmul(h0[..., 2], h0[..., 3], ex, -ey)
+    hr, hi = ar + br, ai + bi
+    ihr, ihi = -hi, hr
+    ydx = (ihr * kx, ihi * kx)
+    ydz = (ihr * kz, ihi * kz)
+    dx = (ydx[0] * ik, ydx[1] * ik)
+    dz = (ydz[0] * ik, ydz[1] * ik)
+    aux = (-hr * ik, -hi * ik)
+    dxdx = (aux[0] * kx * kx, aux[1] * kx * kx)
+    dzdz = (aux[0] * kz * kz, aux[1] * kz * kz)
+    dzdx = (aux[0] * kx * kz, aux[1] * kx * kz)
+    planes = [(dx[0] - dz[1], dx[1] + dz[0]), (hr - dzdx[1], hi + dzdx[0]),
+              (ydx[0] - ydz[1], ydx[1] + ydz[0]), (dxdx[0] - dzdz[1], dxdx[1] + dzdz[0])]
+
+    # butterfly texture: PrecomputeTwiddleFactorsAndInputIndices
+    tab = np.zeros((logn, n, 4), np.float32)
+    mult = f(2) * f(3.14159265) / f(n)
+    for s in range(logn):
+        b = n >> (s + 1)
+        j = np.arange(n // 2)
+        i = (2 * b * (j // b) + j % b) % n
+        arg = -mult * ((j // b) * b).astype(np.float32)
+        tw = (cosf(arg), sinf(arg))  # ComplexExp: exp(-0) = 1
+        tab[s, : n // 2] = np.stack([tw[0], tw[1], i, i + b], -1)
+        tab[s, n // 2:] = np.stack([-tw[0], -tw[1], i, i + b], -1)
+
+    out = []
+    for re_, im_ in planes:
+        for axis in (2, 1):  # HorizontalStepIFFT (index along x), then VerticalStepIFFT (along y)
+            for s in range(logn):
+                wr, wi = tab[s, :, 0], -tab[s, :, 1]
+                i0, i1 = tab[s, :, 2].astype(int), tab[s, :, 3].astype(int)
+                shape = (1, 1, n) if axis == 2 else (1, n, 1)
+                wr, wi = wr.reshape(shape), wi.reshape(shape)
+                br_, bi_ = np.take(re_, i1, axis=axis), np.take(im_, i1, axis=axis)
+                mr, mi = cmul(wr, wi, br_, bi_)
+                re_, im_ = np.take(re_, i0, axis=axis) + mr, np.take(im_, i0, axis=axis) + mi
+        y, x = np.meshgrid(np.arange(n), np.arange(n), indexing="ij")
+        sgn = (f(1) - f(2) * ((x + y) % 2).astype(np.float32))[None]  # Permute
+        out.append((re_ * sgn, im_ * sgn))
+
+    (dxdz_r, dxdz_i), (dydxz_r, dydxz_i), (dyx, dyz), (dxx, dzz) = out
+    disp = np.stack([dxdz_r, dydxz_r, dxdz_i, np.ones_like(dxdz_r)], -1)
+    deriv = np.stack([dyx, dyz, dxx, dzz], -1)
+    jac = (f(1) + dxx) * (f(1) + dzz) - dydxz_i * dydxz_i
+    foam = foam * f(np.exp(-2.0))
+    foam = np.where(foam < jac, foam + jac, foam)
+    return disp, deriv, np.repeat(foam[..., None], 4, -1)
+
+
+@pytest.mark.parametrize("n,cidx,shallow", [(32, [0, 1, 2, 3], False), (16, [0, 1, 2], True)])
+def test_frames_bit_exact_against_numpy_fp32(n, cidx, shallow):
+    """Three consecutive frames of the oracle (evolve, the IFFT of all four planes, fill, foam carried across
+    frames) equal the independent numpy restatement above bit for bit, from the oracle's h0 / waves (pinned bit
+    for bit by the test above).  Times include t = 0 and a large phase."""
+    cosf, sinf = _libm_fp32()
+    noise = O.generate_noise(n, 20251121)
+    cascades = [O.SCENE_CASCADES[i] for i in cidx]
+    oc = O.OracleOcean(n, O.scene_params(shallow), cascades, noise)
+    foam = np.zeros((len(cidx), n, n), np.float32)
+    for t in (0.0, 1.25, 100.0):
+        disp, deriv, turb = oc.step(t)
+        rdisp, rderiv, rturb = _frame_fp32_numpy(oc.h0, oc.waves, t, foam, cosf, sinf)
+        np.testing.assert_array_equal(disp, rdisp)
+        np.testing.assert_array_equal(deriv, rderiv)
+        np.testing.assert_array_equal(turb, rturb)
+        foam = rturb[..., 0]
