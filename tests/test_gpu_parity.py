@@ -1126,3 +1126,76 @@ def test_four_step_column_bands_bit_identical(n, bands):
         np.testing.assert_array_equal(a.read_all(tex), b.read_all(tex))
     a.close()
     b.close()
+
+
+# ------------------------------------------------------------ random scenes
+# Every test above uses the scene of Waves.unity (deep or shallow).  These sweep the physical inputs the
+# WaterBody / WaterCascade inspector exposes (WaterBody.cs:10-14, WaterCascade.cs:10-24), seeded:
+# wind speeds 1-32 m/s, axis-aligned, diagonal, arbitrary and unnormalised wind directions, fetch
+# 300 m-1000 km, depth 0.3-5000 m (every TMA branch), gravity 1-25, cascade wavelengths 10-3000 m with cutoffs
+# that drop low rings or clip the high band, swell and fade over [0, 1], 1-5 cascades, 1-2 tiles,
+# N = 16-1024, full outputs / displacement only / the unfused reference-shaped frame, and times up to
+# 5000 s.  Plus the script defaults (WaterBody.cs:10-14 and WaterCascade.cs:10-24: U10 1, wind (1, 1),
+# fetch 1, depth 4, N 256; L 10, cutoffs 1e-4 / 5, swell 0.4, fade 0.1), which no scene file uses.
+# Checked: noise, wave data and h0 bit-exact; every output channel within the 1e-5 norm-relative tolerance
+# over three frames with the foam carried.
+_AXES = [(1.0, 0.0), (0.0, 1.0), (-1.0, 0.0), (0.0, -1.0), (1.0, 1.0), (3.0, -4.0)]
+
+
+def _random_scene(seed):
+    r = np.random.default_rng(1000 + seed)
+    n = int(r.choice([16, 32, 64, 128, 256, 512, 1024]))
+    C = int(r.integers(1, 6))
+    flags = int(r.choice([0, 0, oh.F_DISPLACEMENT_ONLY, oh.F_UNFUSED]))
+    tiles = int(r.integers(1, 3)) if n <= 256 else 1
+    if r.random() < 0.5:
+        wx, wy = _AXES[int(r.integers(len(_AXES)))]
+    else:
+        a = r.uniform(0, 2 * np.pi)
+        wx, wy = float(np.cos(a)), float(np.sin(a))
+    params = dict(wind_speed=float(10 ** r.uniform(0, 1.5)), wind_dir_x=wx, wind_dir_y=wy,
+                  gravity=float(r.choice([9.81, r.uniform(1.0, 25.0)])), fetch=float(10 ** r.uniform(2.5, 6)),
+                  depth=float(10 ** r.uniform(-0.5, 3.7)))
+    cascades = []
+    for _ in range(C):
+        L = float(10 ** r.uniform(1, 3.5))
+        dk = 2 * np.pi / L
+        cascades.append(dict(wavelength=L, cutoff_low=float(dk * 10 ** r.uniform(-3, 0.8)),
+                             cutoff_high=float(dk * n / 2 * 10 ** r.uniform(-0.8, 1.0)),
+                             swell=float(r.uniform(0, 1)), fade=float(r.uniform(0, 1))))
+    times = [0.0, float(r.uniform(0, 50)), float(r.uniform(100, 5000))]
+    return n, flags, tiles, params, cascades, times
+
+
+SCRIPT_DEFAULTS = (256, 0, 1, dict(wind_speed=1.0, wind_dir_x=1.0, wind_dir_y=1.0, gravity=9.81, fetch=1.0, depth=4.0),
+                   [dict(wavelength=10.0, cutoff_low=1e-4, cutoff_high=5.0, swell=0.4, fade=0.1)], [0.0, 1 / 60, 100.0])
+
+
+@pytest.mark.parametrize("case", ["defaults"] + [f"random{s}" for s in range(30)])
+def test_scene_sweep_vs_oracle(case):
+    n, flags, tiles, params, cascades, times = SCRIPT_DEFAULTS if case == "defaults" else _random_scene(int(case[6:]))
+    seeds = [4242 + t for t in range(tiles)]
+    ctx, noises = make_ctx(n, cascades, params, tiles=tiles, flags=flags, seeds=seeds)
+    nplanes = 2 if flags & oh.F_DISPLACEMENT_ONLY else 4
+    what = f"{case}: n {n} C {len(cascades)} tiles {tiles} flags {flags} params {params}"
+    O.set_threads(oracle_threads() if n >= 512 else 1)
+    try:
+        ocs = []
+        for t, noise in enumerate(noises):
+            h0, waves = O.init_spectrum(n, params, cascades, noise)
+            np.testing.assert_array_equal(ctx.read(oh.TEX_NOISE, t), noise, err_msg=what)
+            np.testing.assert_array_equal(ctx.read_all(oh.TEX_WAVES, t), waves, err_msg=what)
+            np.testing.assert_array_equal(ctx.read_all(oh.TEX_H0, t), h0, err_msg=what)
+            ocs.append(O.OracleOcean(n, params, cascades, noise, nplanes=nplanes))
+        for f, tm in enumerate(times):
+            ctx.step(tm)
+            for t, oc in enumerate(ocs):
+                disp, deriv, turb = oc.step(tm)
+                assert np.isfinite(disp).all(), what
+                assert_channels(ctx.read_all(oh.TEX_DISP, t)[..., :3], disp[..., :3], what=f"{what} tile {t} disp f{f}")
+                if nplanes == 4:
+                    assert_channels(ctx.read_all(oh.TEX_DERIV, t), deriv, what=f"{what} tile {t} deriv f{f}")
+                    assert_channels(ctx.read_all(oh.TEX_TURB, t), turb, what=f"{what} tile {t} turb f{f}")
+    finally:
+        O.set_threads(1)
+    ctx.close()
