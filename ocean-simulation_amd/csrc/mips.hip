@@ -3,9 +3,9 @@
 // texel = ((a + b) + (c + d)) * 0.25 of the 2x2 texels below (ocean.h).
 //
 // k_mips_block: one workgroup per 32x32 block of level 0 of one slice builds
-//   levels 1..5 of that block through LDS (each level 0 texel read once).
+//   levels 1..5 of that block through LDS (each level 0 texel read once; TURB's from the foam state).
 // k_mips_tail: one workgroup per slice builds the remaining levels from level 5.
-// Bytes per texel-cascade: read DERIV + TURB (32 B), write 1/3 of that.
+// Bytes per texel-cascade: read DERIV (16 B) and the foam state (4 B), write 1/3 of 32 B.
 #include <algorithm>
 
 #include "ocean_internal.h"
@@ -20,30 +20,52 @@ __device__ __forceinline__ float4 box(float4 a, float4 b, float4 c, float4 d) {
                        ((a.z + b.z) + (c.z + d.z)) * 0.25f, ((a.w + b.w) + (c.w + d.w)) * 0.25f);
 }
 
+// DERIV's level 0 is read with nontemporal loads: it is read once here, and default-policy loads of its 64 MiB
+// (cfg3) evicted pass A's h0k from the Infinity Cache (pass A 30-35 -> 29 us in the Update loop;
+// docs/MEASUREMENTS.md section 9).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ld_nt(const float4* p) {
+    const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
 __device__ __forceinline__ size_t mip_off(int n, int level) {  // texels before `level` in a chain
     size_t o = 0;
     for (int l = 1; l < level; ++l) o += (size_t)(n >> l) * (n >> l);
     return o;
 }
 
-// grid: (blocks per slice, slices, 2 textures); 256 lanes
+// grid: (blocks per slice, slices, 2 textures); 256 lanes, lane t -> texel (t % h, t / h) of the h x h
+// level-1 block, h = blk / 2.
 __global__ __launch_bounds__(256) void k_mips_block(DevView v, int blk, int levels) {
     const int n = v.n;
     const int tex = blockIdx.z;
-    const float4* src = (tex == 0 ? v.deriv : v.turb) + (size_t)blockIdx.y * n * n;
+    const float4* src = v.deriv + (size_t)blockIdx.y * n * n;
     float4* chain = (tex == 0 ? v.deriv_mips : v.turb_mips) + (size_t)blockIdx.y * v.mip_chain;
     const int bpr = n / blk;  // blocks per row
     const int bx = blockIdx.x % bpr, by = blockIdx.x / bpr;
     __shared__ float4 cur[kBlk / 2 * kBlk / 2];
-    // level 1: lane t -> texel (t % h, t / h) of the h x h level-1 block, h = blk / 2
     int h = blk / 2;
+    const int m1 = n >> 1;
     for (int t = threadIdx.x; t < h * h; t += blockDim.x) {
         const int x = t % h, y = t / h;
         const int X = bx * blk + 2 * x, Y = by * blk + 2 * y;
-        const float4 r = box(src[(size_t)Y * n + X], src[(size_t)Y * n + X + 1], src[(size_t)(Y + 1) * n + X],
-                             src[(size_t)(Y + 1) * n + X + 1]);
-        const int m = n >> 1;
-        chain[mip_off(n, 1) + (size_t)(by * h + y) * m + bx * h + x] = r;
+        float4 r;
+        if (tex == 1) {
+            // TURB is the broadcast RGBA image of the foam state (ResultTexturesFiller.compute:32; every fill and
+            // ocean_write of TURB keeps the two equal), so its level 1 is boxed from the 4-byte state: the same
+            // sums of the same values as boxing TURB's four equal channels, a quarter of the bytes.  State layout
+            // [u][x/W][y][W]: texels X, X + 1 are adjacent in a tile row (X even, W even), row Y + 1 is W on.
+            const int W = v.tile_w;
+            const float* fs = v.foam + (size_t)blockIdx.y * n * n + ((size_t)(X / W) * n + Y) * W + (X % W);
+            const float2 ab = *reinterpret_cast<const float2*>(fs), cd = *reinterpret_cast<const float2*>(fs + W);
+            const float f = ((ab.x + ab.y) + (cd.x + cd.y)) * 0.25f;
+            r = make_float4(f, f, f, f);
+        } else {
+            const float4* p = src + (size_t)Y * n + X;
+            r = box(ld_nt(p), ld_nt(p + 1), ld_nt(p + n), ld_nt(p + n + 1));
+        }
+        chain[mip_off(n, 1) + (size_t)(by * h + y) * m1 + bx * h + x] = r;
         cur[t] = r;
     }
     for (int level = 2; level <= levels; ++level) {
@@ -56,8 +78,7 @@ __global__ __launch_bounds__(256) void k_mips_block(DevView v, int blk, int leve
             const int x = threadIdx.x % h, y = threadIdx.x / h;
             r = box(cur[(2 * y) * hp + 2 * x], cur[(2 * y) * hp + 2 * x + 1], cur[(2 * y + 1) * hp + 2 * x],
                     cur[(2 * y + 1) * hp + 2 * x + 1]);
-            const int m = n >> level;
-            chain[mip_off(n, level) + (size_t)(by * h + y) * m + bx * h + x] = r;
+            chain[mip_off(n, level) + (size_t)(by * h + y) * (n >> level) + bx * h + x] = r;
         }
         __syncthreads();
         if (act) cur[threadIdx.x] = r;
@@ -129,11 +150,12 @@ hipError_t launch_extract_height(const float4* disp_slice, float* dst, size_t te
 }
 
 hipError_t launch_mips(const DevView& v, hipStream_t s) {
-    if (!v.deriv_mips || !v.turb_mips) return hipErrorInvalidValue;
+    if (!v.deriv_mips || !v.turb_mips || !v.foam) return hipErrorInvalidValue;
     const int n = v.n;
     const int blk = n < kBlk ? n : kBlk;
     int levels = 0;
     while ((1 << levels) < blk) ++levels;  // levels 1..log2(blk) from the block kernel
+    if (v.tile_w < 2 || v.tile_w % 2) return hipErrorInvalidValue;  // foam-state texel pairs (k_mips_block)
     const int bps = (n / blk) * (n / blk);
     launch(k_mips_block, dim3(bps, v.units, 2), dim3(256), 0, s, v, blk, levels);
     if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;

@@ -832,6 +832,51 @@ def test_mip_chains_box_filter(n, flags):
     ctx.close()
 
 
+@pytest.mark.parametrize("n,tiles,flags", [(256, 2, 0), (128, 2, oh.F_UNFUSED), (4096, 1, 0)])
+def test_turb_mips_follow_foam_writes_and_resets(n, tiles, flags):
+    """TURB's chain after an ocean_write of TURB with unequal channels (foam resume), after ocean_reset_foam, on
+    every tile, and at N = 4096 (16-wide foam-state tiles): always the box chain of the TURB texture read back."""
+    cas = O.SCENE_CASCADES[:1] if n == 4096 else O.SCENE_CASCADES[:3]
+    ctx, _ = make_ctx(n, cas, tiles=tiles, flags=flags | oh.F_MIPS)
+    rng = np.random.default_rng(5)
+
+    def check(what):
+        for t in range(tiles):
+            for c in range(len(cas)):
+                turb = ctx.read(oh.TEX_TURB, t, c)
+                assert (turb == turb[..., :1]).all(), what  # the fill writes the foam broadcast
+                for level, ref in enumerate(_box_chain(turb), start=1):
+                    np.testing.assert_array_equal(ctx.read_mip(oh.TEX_TURB, level, t, c), ref,
+                                                  err_msg=f"{what} tile {t} cascade {c} level {level}")
+
+    ctx.step(0.25)
+    check("first frame")
+    for t in range(tiles):
+        for c in range(len(cas)):
+            ctx.write(oh.TEX_TURB, rng.uniform(-1, 3, (n, n, 4)).astype(np.float32), t, c)
+    ctx.step(0.5)
+    check("after ocean_write(TURB)")
+    ctx.reset_foam()
+    ctx.step(0.75)
+    check("after ocean_reset_foam")
+    ctx.close()
+
+
+def test_mips_after_many_frames():
+    """After 64 frames of 8 slices (2 tiles x 4 cascades at 1024^2; TURB's chain boxed from the foam state,
+    csrc/mips.hip) every level of every chain is the box chain of its level 0."""
+    ctx, _ = make_ctx(1024, O.SCENE_CASCADES, tiles=2, flags=oh.F_MIPS)
+    for f in range(64):
+        ctx.step(f / 60.0)
+    for tex in (oh.TEX_DERIV, oh.TEX_TURB):
+        for t in range(2):
+            for c in range(len(O.SCENE_CASCADES)):
+                for level, ref in enumerate(_box_chain(ctx.read(tex, t, c)), start=1):
+                    np.testing.assert_array_equal(ctx.read_mip(tex, level, t, c), ref,
+                                                  err_msg=f"tex {tex} tile {t} cascade {c} level {level}")
+    ctx.close()
+
+
 def test_mip_errors():
     ctx, _ = make_ctx(32, O.SCENE_CASCADES[:1])
     with pytest.raises(oh.OceanError) as e:
