@@ -655,6 +655,30 @@ def test_height_readback_matches_rgba():
         wb.OnDisable()
 
 
+@pytest.mark.parametrize("flags", [oh.F_MIPS, 0, oh.F_UNFUSED])
+def test_height_readback_snapshots_behind_later_steps(flags):
+    """Snapshot semantics of ocean_read_height_async: each request, made with later steps and an ocean_write of
+    DISP queued right behind it, still holds DISP.y of its own frame, bit for bit (DISP depends on t only: a
+    second context gives it), with and without the mips, fused and unfused."""
+    n, cas = 256, O.SCENE_CASCADES[:2]
+    ctx, _ = make_ctx(n, cas, flags=flags)
+    ref, _ = make_ctx(n, cas, flags=flags)
+    times = [0.1 * k for k in range(8)]
+    reqs = []
+    for k, t in enumerate(times):
+        ctx.step(t)
+        reqs.append(ctx.read_height_async(0, k % len(cas)))
+        if k == 5:  # DISP overwritten right behind a request
+            ctx.write(oh.TEX_DISP, np.zeros((n, n, 4), np.float32), 0, k % len(cas))
+    ctx.synchronize()
+    for k, (t, rb) in enumerate(zip(times, reqs)):
+        ref.step(t)
+        np.testing.assert_array_equal(rb.data, ref.read(oh.TEX_DISP, 0, k % len(cas))[..., 1], err_msg=f"frame {k}")
+        rb.release()
+    ctx.close()
+    ref.close()
+
+
 def test_state_errors():
     ctx = oh.OceanContext(64, 1, 1)
     with pytest.raises(oh.OceanError) as ei:
